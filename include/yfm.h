@@ -1,0 +1,113 @@
+/*
+ * yfm.h — C ABI of libyfm_hip.so: the batched Kalman-filter log-likelihood of
+ * YieldFactorModels.jl on MI355X (gfx950).
+ *
+ * The reference has no FFI on this path; its plug-in point is Julia multiple
+ * dispatch.  Each entry point below names the reference function it replaces
+ * (paths relative to the reference root) — the Julia-side `@ccall` binding a
+ * maintainer would add is in INTEGRATION.md.
+ *
+ * Conventions
+ *   - All arrays are plain host (or, for *_device, device) pointers with explicit
+ *     sizes.  Matrices are column-major like Julia's: the panel Y is N×T
+ *     (rows = maturities, columns = months, data_management.jl:1-5) and a batch
+ *     of parameter vectors Θ is P×B (candidate b is Θ[:, b], contiguous).
+ *   - FP64 throughout (the reference's Float64 path, test.jl:25).
+ *   - Return value: YFM_OK (0) or a negative yfm_status; yfm_last_error() then
+ *     holds a thread-local message.  Numeric failures of one candidate are NOT
+ *     errors: they are written into that candidate's output (see below).
+ *   - A context is bound to one HIP device and is not thread-safe; use one
+ *     context per host thread / per GPU.  Host-pointer calls are synchronous.
+ *
+ * Per-candidate numeric semantics (bitwise the reference's values)
+ *   loglik_out[b] = +loglik as returned by get_loss (filter.jl:182-209):
+ *     -Inf  where the reference returns -Inf (det F < 0 at t ≥ 2: DomainError in
+ *           logdet, filter.jl:197-200; any non-finite loglik, filter.jl:202-204);
+ *     NaN   where the reference would THROW from initialize_filter (singular
+ *           I − Φ or I − Φ⊗Φ, filter.jl:4,7) — counted in n_init_throw.
+ */
+#ifndef YFM_H
+#define YFM_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define YFM_ABI_VERSION 1
+
+typedef struct yfm_ctx yfm_ctx;
+
+/* model_kind — create_model codes (src/model_dictionary.jl:11-16) */
+enum yfm_model_kind {
+  YFM_MODEL_DNS = 0,  /* "1C" / "0": DNSModel, fixed λ, M = 3, P = 20 (dns.jl) */
+  YFM_MODEL_TVL = 1,  /* "TVλ" / "1": TVλDNSModel EKF, M = 4, P = 31 (tvλdns.jl) */
+  YFM_MODEL_GNS5 = 2  /* extension, not in the reference: 5-factor generalised NS, M = 5, P = 48 */
+};
+
+/* param_space */
+enum yfm_param_space {
+  YFM_THETA_UNCONSTRAINED = 0, /* θ as compute_loss receives it (optimization.jl:10-23) */
+  YFM_THETA_CONSTRAINED = 1    /* θ_c as set_params! receives it (paramoperations.jl:6-68) */
+};
+
+enum yfm_status {
+  YFM_OK = 0,
+  YFM_EINVAL = -1,      /* bad argument (sizes, kind, pointer) */
+  YFM_EHIP = -2,        /* HIP runtime error */
+  YFM_ENOPANEL = -3,    /* no panel set on this context */
+  YFM_EUNSUPPORTED = -4 /* valid request this build has no kernel for */
+};
+
+/* Library/ABI introspection. */
+int yfm_abi_version(void);
+/* Length P of θ for a model kind (kalmanbasemodel.jl:106-112 + dns.jl:15-22). */
+int yfm_param_count(int model_kind);
+/* State dimension M (3 DNS, 4 TVλ, 5 GNS5). */
+int yfm_state_dim(int model_kind);
+/* Thread-local message for the last failing call on this thread ("" if none). */
+const char* yfm_last_error(void);
+
+/* Context lifetime.  Replaces the per-model preallocated buffers of
+ * KalmanBaseModel (kalmanbasemodel.jl:46-130): device buffers live in the ctx. */
+yfm_ctx* yfm_create(int hip_device);
+void yfm_destroy(yfm_ctx* ctx);
+
+/* Upload the yield panel.  Y: N×T column-major (the `data` argument of get_loss,
+ * filter.jl:182); maturities: N (KalmanBaseModel.maturities).  Copied; the
+ * caller keeps ownership.  NaN columns are allowed (prediction-only steps). */
+int yfm_set_panel(yfm_ctx* ctx, const double* Y, int N, int T, const double* maturities);
+
+/* Batched log-likelihood — replaces B calls of
+ *   compute_loss(model, data, θ_b)  (optimization.jl:10-23; loglik = -loss) when
+ *   param_space = YFM_THETA_UNCONSTRAINED, or
+ *   set_params!(model, θ_b); get_loss(model, data)  (filter.jl:182-209)
+ *   when param_space = YFM_THETA_CONSTRAINED.
+ * theta: P×B column-major.  T_use: NULL (every candidate uses all T columns) or
+ * B window lengths, candidate b then evaluates get_loss(model, data[:, 1:T_use[b]])
+ * (the expanding-window re-estimation of forecasting.jl:140-176), 1 ≤ T_use[b] ≤ T.
+ * loglik_out: B doubles.  Synchronous. */
+int yfm_loglik_batch(yfm_ctx* ctx, int model_kind, int param_space, const double* theta, int P, int B,
+                     const int* T_use, double* loglik_out);
+
+/* Same with DEVICE pointers on the caller's HIP stream (hipStream_t passed as
+ * void*, NULL = default stream); asynchronous: returns after enqueueing.  For
+ * pipelines that keep Θ resident in HBM (bench.py, RCCL sharding). */
+int yfm_loglik_batch_device(yfm_ctx* ctx, int model_kind, int param_space, const double* d_theta, int P, int B,
+                            const int* d_T_use, double* d_loglik_out, void* hip_stream);
+
+/* Filtered-state trajectories for parity checks: after every filter! call t
+ * (t = 1..T-1), beta and P hold a_{t+1|t}, P_{t+1|t} (filter.jl:125-179).
+ * beta_out: M × (T-1) × B, P_out: M × M × (T-1) × B (column-major), loglik_out: B.
+ * Meant for small B (the output is O(B·T·M²)).  Synchronous. */
+int yfm_filter_states(yfm_ctx* ctx, int model_kind, int param_space, const double* theta, int P, int B,
+                      const int* T_use, double* beta_out, double* P_out, double* loglik_out);
+
+/* Counters of the last completed batch on this ctx: candidates where the
+ * reference would have thrown (NaN outputs) and candidates returning -Inf.
+ * For yfm_loglik_batch_device, synchronise the stream first. */
+int yfm_last_batch_flags(yfm_ctx* ctx, long long* n_init_throw, long long* n_neg_inf);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* YFM_H */

@@ -1,0 +1,169 @@
+"""GPU parity: libyfm_hip.so (through the C ABI) vs the oracle / committed golden fixtures.
+
+Tolerance (north star, BASELINE.json): 1e-9 relative on loglik and on the filtered
+states, FP64; -Inf / NaN patterns must match exactly.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN_NAMES, ROOT, load_golden
+from yfm_amd import KIND_DNS, KIND_GNS, KIND_TVL, _lib
+from yfm_amd import synthetic as S
+
+pytestmark = pytest.mark.gpu
+
+REL = 1e-9
+
+
+def assert_ll_close(got, ref, rel=REL):
+    got, ref = np.asarray(got), np.asarray(ref)
+    assert np.array_equal(np.isnan(got), np.isnan(ref)), (got, ref)
+    assert np.array_equal(np.isneginf(got), np.isneginf(ref)), (got, ref)
+    assert not np.isposinf(got).any()
+    fin = np.isfinite(ref)
+    if fin.any():
+        err = np.abs(got[fin] - ref[fin]) / np.maximum(np.abs(ref[fin]), 1e-300)
+        # loglik exactly 0.0 (T_use ≤ 2) must be exact
+        assert np.all((ref[fin] != 0.0) | (got[fin] == 0.0))
+        assert err.max() <= rel, (err.max(), np.argmax(err))
+
+
+def supported(kind):
+    return kind != KIND_TVL
+
+
+@pytest.mark.parametrize("name", GOLDEN_NAMES)
+def test_golden_loglik(engine, name):
+    g = load_golden(name)
+    kind = int(g["kind"])
+    if not supported(kind):
+        pytest.skip("TVλ kernel not built yet")
+    engine.set_panel(g["Y"], g["maturities"])
+    got = engine.loglik(kind, g["Theta"], space=int(g["space"]), T_use=g.get("T_use"))
+    assert_ll_close(got, g["loglik"])
+
+
+@pytest.mark.parametrize("name", [n for n in GOLDEN_NAMES if "beta_traj" in load_golden(n)])
+def test_golden_states(engine, name):
+    g = load_golden(name)
+    kind = int(g["kind"])
+    if not supported(kind):
+        pytest.skip("TVλ kernel not built yet")
+    engine.set_panel(g["Y"], g["maturities"])
+    nt = g["beta_traj"].shape[-1]
+    ll, beta, P = engine.filter_states(kind, g["Theta"][:, :nt], space=int(g["space"]))
+    assert_ll_close(ll, g["loglik"][:nt])
+    for b in range(nt):
+        if not np.isfinite(g["loglik"][b]):
+            continue
+        rb, rP = g["beta_traj"][..., b], g["P_traj"][..., b]
+        np.testing.assert_allclose(beta[..., b], rb, rtol=REL, atol=REL * np.abs(rb).max())
+        np.testing.assert_allclose(P[..., b], rP, rtol=REL, atol=REL * np.abs(rP).max())
+
+
+@pytest.fixture(scope="module")
+def headline():
+    Y = S.simulate_panel(KIND_DNS, 600)
+    return Y, S.maturities_30()
+
+
+def test_headline_shape_vs_c_oracle(engine, headline):
+    """N = 30, T = 600 (config 1/2 shape), 256 candidates incl. 1% non-stationary Φ, vs the C oracle."""
+    import ctypes
+    Y, mats = headline
+    Th = S.theta_batch(KIND_DNS, 256, seed=99, bad_frac=0.05)
+    engine.set_panel(Y, mats)
+    got = engine.loglik(KIND_DNS, Th)
+    lib = ctypes.CDLL(str(ROOT / "oracle" / "libyfm_oracle.so"))
+    D = ctypes.POINTER(ctypes.c_double)
+    ref = np.empty(256)
+    Yf = np.asfortranarray(Y)
+    lib.yfm_oracle_loglik(KIND_DNS, 0, Yf.ctypes.data_as(D), 30, 600, mats.ctypes.data_as(D),
+                          Th.ctypes.data_as(D), 20, 256, None, ref.ctypes.data_as(D), 0)
+    assert_ll_close(got, ref)
+
+
+def test_full_batch_properties(engine, headline):
+    """B = 65,536 (config 2): results are independent of batch position and size, deterministic, and the
+    flag counters match the NaN/-Inf outputs."""
+    Y, mats = headline
+    engine.set_panel(Y, mats)
+    Th = S.theta_batch(KIND_DNS, 65536)
+    a = engine.loglik(KIND_DNS, Th)
+    n_throw, n_neginf = engine.last_flags()
+    assert n_throw == np.isnan(a).sum() and n_neginf == np.isneginf(a).sum()
+    b = engine.loglik(KIND_DNS, Th)
+    np.testing.assert_array_equal(a, b)  # bit-deterministic
+    perm = np.random.default_rng(1).permutation(65536)[:1000]
+    c = engine.loglik(KIND_DNS, np.asfortranarray(Th[:, perm]))
+    np.testing.assert_array_equal(c, a[perm])  # position/size independent
+    assert np.isfinite(a).mean() > 0.95
+
+
+def test_constrained_equals_unconstrained(engine, headline):
+    from yfm_amd.params import transform_params
+    Y, mats = headline
+    engine.set_panel(Y[:, :200], mats)
+    Th = S.theta_batch(KIND_DNS, 64, seed=4, bad_frac=0.0)
+    a = engine.loglik(KIND_DNS, Th, space=0)
+    b = engine.loglik(KIND_DNS, transform_params(KIND_DNS, Th), space=1)
+    assert_ll_close(a, b, rel=1e-12)
+
+
+def test_device_pointer_api_matches_host_api(engine, headline):
+    import torch
+    Y, mats = headline
+    engine.set_panel(Y, mats)
+    Th = S.theta_batch(KIND_DNS, 4096, seed=8)
+    ref = engine.loglik(KIND_DNS, Th)
+    dth = torch.from_numpy(np.ascontiguousarray(Th.T)).cuda()  # (B, P) C-order == P×B column-major
+    out = torch.empty(4096, dtype=torch.float64, device="cuda")
+    s = torch.cuda.current_stream()
+    engine.loglik_device(KIND_DNS, dth.data_ptr(), 20, 4096, out.data_ptr(), space=0, stream=s.cuda_stream)
+    s.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+
+
+def test_windows_share_prefix(engine, headline):
+    """T_use windows: candidate with T_use = τ equals a full evaluation on data[:, :τ]."""
+    Y, mats = headline
+    Th = S.theta_batch(KIND_DNS, 8, seed=21, bad_frac=0.0)
+    Th = np.asfortranarray(np.repeat(Th, 3, axis=1))
+    tu = np.array([361, 480, 600] * 8, dtype=np.int32)
+    engine.set_panel(Y, mats)
+    got = engine.loglik(KIND_DNS, Th, T_use=tu)
+    for tau in (361, 480, 600):
+        engine.set_panel(Y[:, :tau], mats)
+        ref = engine.loglik(KIND_DNS, Th[:, tu == tau])
+        np.testing.assert_array_equal(got[tu == tau], ref)
+
+
+def test_edge_sizes(engine, headline):
+    Y, mats = headline
+    engine.set_panel(Y[:, :1], mats)
+    np.testing.assert_array_equal(engine.loglik(KIND_DNS, S.theta_batch(KIND_DNS, 3, bad_frac=0.0)), 0.0)
+    engine.set_panel(Y[:, :50], mats)
+    assert engine.loglik(KIND_DNS, np.zeros((20, 0))).shape == (0,)
+    with pytest.raises(_lib.YFMError):
+        engine.loglik(KIND_DNS, np.zeros((19, 4)))  # wrong P
+    with pytest.raises(_lib.YFMError):
+        engine.loglik(KIND_DNS, np.zeros((20, 2)), T_use=np.array([0, 5]))
+
+
+def test_model_api_mirror(engine, headline):
+    """create_model / set_params_ / get_loss / compute_loss mirror the reference's call sequence."""
+    from oracle import kalman_oracle as O
+    from yfm_amd import compute_loss, compute_loss_batch, create_model, get_loss, set_params_
+    Y, mats = headline
+    Y = Y[:, :150]
+    model, _ = create_model("1C", mats, 30, 3)
+    th = S.theta0(KIND_DNS)
+    ref = O.loglik(KIND_DNS, mats, 3, Y, th)
+    assert abs(-compute_loss(model, Y, th) - ref) <= REL * abs(ref)
+    set_params_(model, S.theta0_constrained(KIND_DNS))
+    assert abs(get_loss(model, Y) - ref) <= 1e-9 * abs(ref)
+    Th = S.theta_batch(KIND_DNS, 16, seed=2, bad_frac=0.0)
+    cl = compute_loss_batch(model, Y, Th)
+    assert abs(-cl[0] - O.loglik(KIND_DNS, mats, 3, Y, Th[:, 0])) <= REL * abs(cl[0])

@@ -1,0 +1,131 @@
+"""CPU tests of the oracle itself: pinned by closed-form known answers (no filter
+code involved) and by agreement of the two independent restatements
+(oracle/kalman_oracle.py — NumPy+LAPACK; oracle/yfm_oracle.c — own getrf/getri)."""
+from __future__ import annotations
+
+import ctypes
+import math
+import subprocess
+
+import numpy as np
+import pytest
+from scipy.stats import multivariate_normal
+
+from conftest import GOLDEN_NAMES, ROOT, load_golden
+from oracle import kalman_oracle as O
+from yfm_amd import synthetic as S
+from yfm_amd.params import KIND_DNS, KIND_GNS, KIND_TVL, param_layout, state_dim
+
+REL = 1e-9
+
+
+@pytest.fixture(scope="module")
+def coracle():
+    lib_path = ROOT / "oracle" / "libyfm_oracle.so"
+    if not lib_path.exists():
+        subprocess.run(["make", "-C", str(ROOT / "oracle"), "-s"], check=True)
+    lib = ctypes.CDLL(str(lib_path))
+    D = ctypes.POINTER(ctypes.c_double)
+
+    def run(kind, Y, mats, Th, space=0, T_use=None, nthreads=4):
+        Y = np.asfortranarray(Y, dtype=np.float64)
+        Th = np.asfortranarray(Th, dtype=np.float64)
+        mats = np.ascontiguousarray(mats, dtype=np.float64)
+        B = Th.shape[1]
+        out = np.empty(B)
+        tu = None if T_use is None else np.ascontiguousarray(T_use, dtype=np.int32)
+        rc = lib.yfm_oracle_loglik(kind, space, Y.ctypes.data_as(D), Y.shape[0], Y.shape[1], mats.ctypes.data_as(D),
+                                   Th.ctypes.data_as(D), Th.shape[0], B,
+                                   None if tu is None else tu.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+                                   out.ctypes.data_as(D), nthreads)
+        assert rc == 0
+        return out
+    return run
+
+
+def rel_err(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    fa, fb = np.isfinite(a), np.isfinite(b)
+    assert np.array_equal(fa, fb), (a, b)
+    assert np.array_equal(np.isnan(a), np.isnan(b)), (a, b)
+    assert np.array_equal(np.isneginf(a), np.isneginf(b)), (a, b)
+    if not fa.any():
+        return 0.0
+    return float(np.max(np.abs(a[fa] - b[fa]) / np.maximum(np.abs(b[fa]), 1e-300)))
+
+
+def test_known_answer_iid():
+    """Φ = 0 ⇒ β_{t|t-1} = δ, P_{t|t-1} = Q: loglik = Σ_{t=2}^{T-1} log N(y_t; Zδ, ZQZ'+σ²I) (filter.jl:190-195)."""
+    mats = S.maturities_30()
+    Y = S.simulate_panel(KIND_DNS, 60)
+    tc = S.theta0_constrained(KIND_DNS)
+    lay = param_layout(KIND_DNS)
+    tc[lay.phi_offset:lay.phi_offset + 9] = 0.0
+    ll = O.loglik(KIND_DNS, mats, 3, Y, tc, space=1)
+    s = O.KalmanState.fresh(KIND_DNS, mats, 3)
+    O.set_params(s, tc)
+    F = s.Z @ s.Omega_state @ s.Z.T + s.Omega_obs
+    ka = sum(multivariate_normal.logpdf(Y[:, t], s.Z @ s.delta, F) for t in range(1, 59))
+    assert abs(ll - ka) <= 1e-12 * abs(ka)
+
+
+def test_known_answer_scalar_closed_form():
+    """N = 1, Φ = 0 and a constant panel: every term is the same closed-form N(y; z'δ, z'Qz + σ²)."""
+    mats = np.array([12.0])
+    tc = S.theta0_constrained(KIND_DNS)
+    lay = param_layout(KIND_DNS)
+    tc[lay.phi_offset:lay.phi_offset + 9] = 0.0
+    Y = np.full((1, 25), 4.2)
+    ll = O.loglik(KIND_DNS, mats, 3, Y, tc, space=1)
+    s = O.KalmanState.fresh(KIND_DNS, mats, 3)
+    O.set_params(s, tc)
+    z = s.Z[0]
+    var = z @ s.Omega_state @ z + tc[lay.base_offset]
+    mu = z @ s.delta
+    term = -0.5 * (math.log(var) + (4.2 - mu) ** 2 / var + math.log(2 * math.pi))
+    assert abs(ll - 23 * term) <= 1e-12 * abs(23 * term)
+
+
+def test_transform_roundtrip():
+    for kind in (KIND_DNS, KIND_TVL, KIND_GNS):
+        th = S.theta0(kind)
+        codes = O.transform_codes(kind, state_dim(kind))
+        np.testing.assert_allclose(O.untransform_params(codes, O.transform_params(codes, th)), th, rtol=1e-12,
+                                   atol=1e-14)
+
+
+def test_from_R_to_11_overflow_quirk():
+    """transformations.jl:21-26 evaluated as written: exp overflow → Inf/Inf = NaN."""
+    assert math.isnan(O.from_R_to_11(800.0))
+    assert O.from_R_to_11(40.0) == 1.0
+
+
+@pytest.mark.parametrize("name", GOLDEN_NAMES)
+def test_golden_numpy_oracle_reproduces(name):
+    """The committed fixtures are reproducible from the NumPy oracle."""
+    g = load_golden(name)
+    kind = int(g["kind"])
+    B = g["Theta"].shape[1]
+    for b in range(min(B, 6)):
+        Yb = g["Y"] if "T_use" not in g else g["Y"][:, :g["T_use"][b]]
+        ll = O.loglik(kind, g["maturities"], state_dim(kind), Yb, g["Theta"][:, b], space=int(g["space"]))
+        assert rel_err([ll], [g["loglik"][b]]) == 0.0
+
+
+@pytest.mark.parametrize("name", GOLDEN_NAMES)
+def test_golden_c_oracle_agrees(name, coracle):
+    """Independent C restatement (own getrf/getri) vs the NumPy/LAPACK fixtures."""
+    g = load_golden(name)
+    kind = int(g["kind"])
+    out = coracle(kind, g["Y"], g["maturities"], g["Theta"], space=int(g["space"]), T_use=g.get("T_use"))
+    tol = 2e-9 if kind == KIND_TVL else 1e-9  # north-star tolerance; observed ≤ 2e-10
+    assert rel_err(out, g["loglik"]) <= tol
+
+
+def test_c_oracle_headline_batch(coracle):
+    """Headline shape (N = 30, T = 600): C vs NumPy oracle on a handful of candidates incl. bad Φ."""
+    Y = S.simulate_panel(KIND_DNS, 600)
+    Th = S.theta_batch(KIND_DNS, 8, seed=5, bad_frac=0.25)
+    out = coracle(KIND_DNS, Y, S.maturities_30(), Th)
+    ref = [O.loglik(KIND_DNS, S.maturities_30(), 3, Y, Th[:, b]) for b in range(8)]
+    assert rel_err(out, ref) <= 1e-11

@@ -1,0 +1,65 @@
+"""Build libyfm_hip.so (gfx950) in-tree with hipcc — no torch, no JIT cache.
+
+Called by ``__graft_entry__.build()``.  Each translation unit is compiled to an
+object in ``build/`` in parallel, then linked into ``yfm_amd/libyfm_hip.so``.
+A rebuild happens only when a source or header is newer than the library.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+BUILD = PKG / "build"
+LIB = PKG / "yfm_amd" / "libyfm_hip.so"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("YFM_OFFLOAD_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
+         f"-I{ROOT / 'include'}"]
+
+
+def _sources():
+    return sorted(CSRC.glob("*.hip"))
+
+
+def _deps():
+    return list(CSRC.glob("*")) + list((ROOT / "include").glob("*.h")) + [Path(__file__)]
+
+
+def up_to_date() -> bool:
+    if not LIB.exists():
+        return False
+    t = LIB.stat().st_mtime
+    return all(p.stat().st_mtime <= t for p in _deps())
+
+
+def build(force: bool = False, verbose: bool = True) -> Path:
+    if not force and up_to_date():
+        return LIB
+    BUILD.mkdir(exist_ok=True)
+    srcs = _sources()
+    objs = [BUILD / (s.stem + ".o") for s in srcs]
+
+    def cc(pair):
+        s, o = pair
+        cmd = [HIPCC, *FLAGS, "-c", str(s), "-o", str(o)]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+
+    with ThreadPoolExecutor(max_workers=min(len(srcs), 4)) as ex:
+        list(ex.map(cc, zip(srcs, objs)))
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(LIB)]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,286 @@
+// yfm_capi.hip — the C ABI of libyfm_hip.so (declared in include/yfm.h).
+//
+// Owns device memory per context (the panel, staging buffers for the host-pointer
+// entry points, the flag counters) and launches the kernels of yfm_kernels.hip.
+// No torch types, no CPU compute fallback: every result comes from a HIP kernel,
+// and a missing/failed device is reported as an error.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/yfm.h"
+#include "yfm_internal.hpp"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int set_error(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  std::vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+#define YFM_HIP_CHECK(expr)                                                                      \
+  do {                                                                                           \
+    hipError_t _e = (expr);                                                                      \
+    if (_e != hipSuccess) return set_error(YFM_EHIP, "%s: %s", #expr, hipGetErrorString(_e)); \
+  } while (0)
+
+int state_dim(int kind) { return kind == YFM_MODEL_DNS ? 3 : kind == YFM_MODEL_TVL ? 4 : kind == YFM_MODEL_GNS5 ? 5 : -1; }
+int n_lead(int kind) { return kind == YFM_MODEL_DNS ? 1 : kind == YFM_MODEL_TVL ? 0 : 2; }
+int param_count(int kind) {
+  const int M = state_dim(kind);
+  if (M < 0) return -1;
+  return n_lead(kind) + 1 + M * (M + 1) / 2 + M + M * M;
+}
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e == hipSuccess) cap = bytes;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+}  // namespace
+
+struct yfm_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  // panel
+  int N = 0, T = 0, np = 0, ldp = 0;
+  DevBuf panel, mats, raw;
+  // staging for host-pointer calls
+  DevBuf theta, out, tuse, rec_beta, rec_P;
+  DevBuf flags;  // 2 × unsigned int
+};
+
+namespace {
+
+int check_ctx(yfm_ctx* ctx) {
+  if (!ctx) return set_error(YFM_EINVAL, "null context");
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return set_error(YFM_EHIP, "hipSetDevice(%d): %s", ctx->device, hipGetErrorString(e));
+  return YFM_OK;
+}
+
+int check_batch(yfm_ctx* ctx, int kind, int space, int P, int B) {
+  if (state_dim(kind) < 0) return set_error(YFM_EINVAL, "unknown model_kind %d", kind);
+  if (space != YFM_THETA_UNCONSTRAINED && space != YFM_THETA_CONSTRAINED)
+    return set_error(YFM_EINVAL, "unknown param_space %d", space);
+  if (P != param_count(kind))
+    return set_error(YFM_EINVAL, "P = %d but model_kind %d has %d parameters", P, kind, param_count(kind));
+  if (B < 0) return set_error(YFM_EINVAL, "B = %d < 0", B);
+  if (ctx->T <= 0) return set_error(YFM_ENOPANEL, "no panel: call yfm_set_panel first");
+  if (kind == YFM_MODEL_TVL) return set_error(YFM_EUNSUPPORTED, "TVλ kernel not built into this library yet");
+  if (yfm::fixedz_np_for(ctx->N) < 0)
+    return set_error(YFM_EUNSUPPORTED, "N = %d maturities exceeds the fixed-loading kernel's 64", ctx->N);
+  return YFM_OK;
+}
+
+int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int B, const int* d_T_use,
+           double* d_out, double* d_rb, double* d_rP, hipStream_t s) {
+  YFM_HIP_CHECK(hipMemsetAsync(ctx->flags.p, 0, 2 * sizeof(unsigned int), s));
+  if (B == 0) return YFM_OK;
+  yfm::LaunchArgs a;
+  a.theta = d_theta;
+  a.P = P;
+  a.B = B;
+  a.space = space;
+  a.panel = static_cast<const double*>(ctx->panel.p);
+  a.T = ctx->T;
+  a.N = ctx->N;
+  a.np = ctx->np;
+  a.mats = static_cast<const double*>(ctx->mats.p);
+  a.T_use = d_T_use;
+  a.out = d_out;
+  a.flags = static_cast<unsigned int*>(ctx->flags.p);
+  a.rec_beta = d_rb;
+  a.rec_P = d_rP;
+  a.stream = s;
+  hipError_t e = yfm::launch_fixedz(kind, a);
+  if (e != hipSuccess) return set_error(YFM_EHIP, "kernel launch: %s", hipGetErrorString(e));
+  return YFM_OK;
+}
+
+int validate_tuse(const int* T_use, int B, int T) {
+  if (!T_use) return YFM_OK;
+  for (int b = 0; b < B; ++b)
+    if (T_use[b] < 1 || T_use[b] > T)
+      return set_error(YFM_EINVAL, "T_use[%d] = %d outside [1, %d]", b, T_use[b], T);
+  return YFM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int yfm_abi_version(void) { return YFM_ABI_VERSION; }
+int yfm_param_count(int model_kind) { return param_count(model_kind); }
+int yfm_state_dim(int model_kind) { return state_dim(model_kind); }
+const char* yfm_last_error(void) { return g_last_error.c_str(); }
+
+yfm_ctx* yfm_create(int hip_device) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= 0) {
+    set_error(YFM_EHIP, "no HIP device available (%s)", hipGetErrorString(e));
+    return nullptr;
+  }
+  if (hip_device < 0 || hip_device >= n) {
+    set_error(YFM_EINVAL, "hip_device %d out of range [0, %d)", hip_device, n);
+    return nullptr;
+  }
+  if (hipSetDevice(hip_device) != hipSuccess) {
+    set_error(YFM_EHIP, "hipSetDevice(%d) failed", hip_device);
+    return nullptr;
+  }
+  yfm_ctx* ctx = new yfm_ctx();
+  ctx->device = hip_device;
+  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+      ctx->flags.ensure(2 * sizeof(unsigned int)) != hipSuccess) {
+    set_error(YFM_EHIP, "context allocation failed on device %d", hip_device);
+    yfm_destroy(ctx);
+    return nullptr;
+  }
+  (void)hipMemset(ctx->flags.p, 0, 2 * sizeof(unsigned int));
+  return ctx;
+}
+
+void yfm_destroy(yfm_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  for (DevBuf* b : {&ctx->panel, &ctx->mats, &ctx->raw, &ctx->theta, &ctx->out, &ctx->tuse, &ctx->rec_beta,
+                    &ctx->rec_P, &ctx->flags})
+    b->release();
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+int yfm_set_panel(yfm_ctx* ctx, const double* Y, int N, int T, const double* maturities) {
+  if (int r = check_ctx(ctx)) return r;
+  if (!Y || !maturities) return set_error(YFM_EINVAL, "null Y or maturities");
+  if (N < 1 || T < 1) return set_error(YFM_EINVAL, "N = %d, T = %d must be >= 1", N, T);
+  const int np = yfm::fixedz_np_for(N);
+  const int npad = np > 0 ? np : ((N + 7) / 8) * 8;
+  const int ldp = npad + 4;
+  YFM_HIP_CHECK(ctx->raw.ensure(sizeof(double) * (size_t)N * T));
+  YFM_HIP_CHECK(ctx->panel.ensure(sizeof(double) * (size_t)ldp * T));
+  YFM_HIP_CHECK(ctx->mats.ensure(sizeof(double) * (size_t)N));
+  YFM_HIP_CHECK(hipMemcpyAsync(ctx->raw.p, Y, sizeof(double) * (size_t)N * T, hipMemcpyHostToDevice, ctx->stream));
+  YFM_HIP_CHECK(hipMemcpyAsync(ctx->mats.p, maturities, sizeof(double) * N, hipMemcpyHostToDevice, ctx->stream));
+  YFM_HIP_CHECK(yfm::launch_prep_panel(static_cast<const double*>(ctx->raw.p), N, T, npad, ldp,
+                                       static_cast<double*>(ctx->panel.p), ctx->stream));
+  YFM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+  ctx->N = N;
+  ctx->T = T;
+  ctx->np = npad;
+  ctx->ldp = ldp;
+  return YFM_OK;
+}
+
+int yfm_loglik_batch(yfm_ctx* ctx, int model_kind, int param_space, const double* theta, int P, int B,
+                     const int* T_use, double* loglik_out) {
+  if (int r = check_ctx(ctx)) return r;
+  if (int r = check_batch(ctx, model_kind, param_space, P, B)) return r;
+  if (B > 0 && (!theta || !loglik_out)) return set_error(YFM_EINVAL, "null theta or loglik_out");
+  if (int r = validate_tuse(T_use, B, ctx->T)) return r;
+  const size_t nb = (size_t)(B > 0 ? B : 1);
+  YFM_HIP_CHECK(ctx->theta.ensure(sizeof(double) * (size_t)P * nb));
+  YFM_HIP_CHECK(ctx->out.ensure(sizeof(double) * nb));
+  if (B > 0)
+    YFM_HIP_CHECK(hipMemcpyAsync(ctx->theta.p, theta, sizeof(double) * (size_t)P * B, hipMemcpyHostToDevice,
+                                 ctx->stream));
+  const int* d_tuse = nullptr;
+  if (T_use && B > 0) {
+    YFM_HIP_CHECK(ctx->tuse.ensure(sizeof(int) * nb));
+    YFM_HIP_CHECK(hipMemcpyAsync(ctx->tuse.p, T_use, sizeof(int) * B, hipMemcpyHostToDevice, ctx->stream));
+    d_tuse = static_cast<const int*>(ctx->tuse.p);
+  }
+  if (int r = launch(ctx, model_kind, param_space, static_cast<const double*>(ctx->theta.p), P, B, d_tuse,
+                     static_cast<double*>(ctx->out.p), nullptr, nullptr, ctx->stream))
+    return r;
+  if (B > 0)
+    YFM_HIP_CHECK(hipMemcpyAsync(loglik_out, ctx->out.p, sizeof(double) * B, hipMemcpyDeviceToHost, ctx->stream));
+  YFM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+  return YFM_OK;
+}
+
+int yfm_loglik_batch_device(yfm_ctx* ctx, int model_kind, int param_space, const double* d_theta, int P, int B,
+                            const int* d_T_use, double* d_loglik_out, void* hip_stream) {
+  if (int r = check_ctx(ctx)) return r;
+  if (int r = check_batch(ctx, model_kind, param_space, P, B)) return r;
+  if (B > 0 && (!d_theta || !d_loglik_out)) return set_error(YFM_EINVAL, "null d_theta or d_loglik_out");
+  return launch(ctx, model_kind, param_space, d_theta, P, B, d_T_use, d_loglik_out, nullptr, nullptr,
+                static_cast<hipStream_t>(hip_stream));
+}
+
+int yfm_filter_states(yfm_ctx* ctx, int model_kind, int param_space, const double* theta, int P, int B,
+                      const int* T_use, double* beta_out, double* P_out, double* loglik_out) {
+  if (int r = check_ctx(ctx)) return r;
+  if (int r = check_batch(ctx, model_kind, param_space, P, B)) return r;
+  if (B > 0 && (!theta || !beta_out || !P_out || !loglik_out)) return set_error(YFM_EINVAL, "null pointer argument");
+  if (int r = validate_tuse(T_use, B, ctx->T)) return r;
+  if (B == 0 || ctx->T < 2) {
+    return yfm_loglik_batch(ctx, model_kind, param_space, theta, P, B, T_use, loglik_out);
+  }
+  const int M = state_dim(model_kind);
+  const size_t steps = (size_t)(ctx->T - 1) * B;
+  YFM_HIP_CHECK(ctx->theta.ensure(sizeof(double) * (size_t)P * B));
+  YFM_HIP_CHECK(ctx->out.ensure(sizeof(double) * B));
+  YFM_HIP_CHECK(ctx->rec_beta.ensure(sizeof(double) * steps * M));
+  YFM_HIP_CHECK(ctx->rec_P.ensure(sizeof(double) * steps * M * M));
+  YFM_HIP_CHECK(hipMemsetAsync(ctx->rec_beta.p, 0xff, sizeof(double) * steps * M, ctx->stream));  // NaN fill
+  YFM_HIP_CHECK(hipMemsetAsync(ctx->rec_P.p, 0xff, sizeof(double) * steps * M * M, ctx->stream));
+  YFM_HIP_CHECK(hipMemcpyAsync(ctx->theta.p, theta, sizeof(double) * (size_t)P * B, hipMemcpyHostToDevice,
+                               ctx->stream));
+  const int* d_tuse = nullptr;
+  if (T_use) {
+    YFM_HIP_CHECK(ctx->tuse.ensure(sizeof(int) * B));
+    YFM_HIP_CHECK(hipMemcpyAsync(ctx->tuse.p, T_use, sizeof(int) * B, hipMemcpyHostToDevice, ctx->stream));
+    d_tuse = static_cast<const int*>(ctx->tuse.p);
+  }
+  if (int r = launch(ctx, model_kind, param_space, static_cast<const double*>(ctx->theta.p), P, B, d_tuse,
+                     static_cast<double*>(ctx->out.p), static_cast<double*>(ctx->rec_beta.p),
+                     static_cast<double*>(ctx->rec_P.p), ctx->stream))
+    return r;
+  YFM_HIP_CHECK(hipMemcpyAsync(loglik_out, ctx->out.p, sizeof(double) * B, hipMemcpyDeviceToHost, ctx->stream));
+  YFM_HIP_CHECK(hipMemcpyAsync(beta_out, ctx->rec_beta.p, sizeof(double) * steps * M, hipMemcpyDeviceToHost,
+                               ctx->stream));
+  YFM_HIP_CHECK(hipMemcpyAsync(P_out, ctx->rec_P.p, sizeof(double) * steps * M * M, hipMemcpyDeviceToHost,
+                               ctx->stream));
+  YFM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+  return YFM_OK;
+}
+
+int yfm_last_batch_flags(yfm_ctx* ctx, long long* n_init_throw, long long* n_neg_inf) {
+  if (int r = check_ctx(ctx)) return r;
+  unsigned int h[2] = {0, 0};
+  YFM_HIP_CHECK(hipMemcpy(h, ctx->flags.p, sizeof(h), hipMemcpyDeviceToHost));
+  if (n_init_throw) *n_init_throw = h[0];
+  if (n_neg_inf) *n_neg_inf = h[1];
+  return YFM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,336 @@
+// yfm_device.hpp — device-side building blocks for the batched Kalman log-likelihood.
+//
+// Everything here is per-lane FP64 scalar code on fixed-size (compile-time M)
+// arrays: the compiler fully unrolls it and keeps the state in VGPRs.  Row/column
+// pivot choices are runtime values, realised as selects (no scratch indexing).
+//
+// Reference semantics restated (paths relative to the reference root):
+//   decode_params    src/models/parameteroperations.jl:22-32 (transform_params),
+//                    src/models/kalman/kalmanbasemodel.jl:74-120 (transform order),
+//                    src/models/kalman/paramoperations.jl:6-59 (set_params!),
+//                    src/utils/transformations.jl:2-26
+//   init_state       src/models/kalman/filter.jl:1-10 (initialize_filter)
+//   capacitance_*    the F = ZPZ' + σ²I solve of filter.jl:147-176 in capacitance
+//                    (Woodbury) form: see DESIGN.md §3 for the algebra.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace yfm {
+
+constexpr double kLog2Pi = 1.8378770664093454835606594728112;  // log(2π)
+constexpr double kLn2 = 0.69314718055994530941723212145818;
+
+__device__ __forceinline__ double from_R_to_11(double x) {
+  // transformations.jl:21-26, evaluated exactly as written (x > ~709.78 gives Inf/Inf = NaN)
+  const double y = exp(x);
+  return 2.0 * y / (1.0 + y) - 1.0;
+}
+
+template <int M, int LEAD>
+struct Params {
+  double gam[LEAD > 0 ? LEAD : 1];
+  double sigma2;
+  double Q[M][M];
+  double delta[M];
+  double Phi[M][M];
+};
+
+constexpr int param_count(int M, int lead) { return lead + 1 + M * (M + 1) / 2 + M + M * M; }
+
+// transform_params (space == 0) + set_params!: θ layout [γ…, σ², U by column (i ≤ j), δ, Φ row-major].
+template <int M, int LEAD>
+__device__ __forceinline__ void decode_params(const double* __restrict__ th, int space, Params<M, LEAD>& p) {
+  int k = 0;
+#pragma unroll
+  for (int l = 0; l < LEAD; ++l) p.gam[l] = th[k++];
+  p.sigma2 = space == 0 ? exp(th[k]) : th[k];
+  ++k;
+  double U[M][M];
+#pragma unroll
+  for (int j = 0; j < M; ++j) {
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      if (i <= j) {
+        double x = th[k++];
+        if (i == j && space == 0) x = exp(x);
+        U[i][j] = x;
+      } else {
+        U[i][j] = 0.0;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < M; ++i)
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      double s = 0.0;
+#pragma unroll
+      for (int l = 0; l < M; ++l) s = fma(U[l][i], U[l][j], s);  // Q = U'U (paramoperations.jl:35)
+      p.Q[i][j] = s;
+    }
+#pragma unroll
+  for (int i = 0; i < M; ++i) p.delta[i] = th[k++];
+#pragma unroll
+  for (int i = 0; i < M; ++i)
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      double x = th[k++];
+      if (i == j && space == 0) x = from_R_to_11(x);
+      p.Phi[i][j] = x;  // reshape(·, M, M)' == row-major (paramoperations.jl:38)
+    }
+}
+
+// In-register Gaussian elimination with partial pivoting (LAPACK getf2 pivot rule:
+// first index of max |a|), n×n with R right-hand sides.  Returns false on an exact
+// zero pivot — where LAPACK's getrf reports info > 0 and Julia throws.
+template <int n, int R>
+__device__ __forceinline__ bool gauss_solve(double (&A)[n][n], double (&X)[n][R]) {
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < n; ++k) {
+    // pivot search
+    int p = k;
+    double amax = fabs(A[k][k]);
+#pragma unroll
+    for (int i = k + 1; i < n; ++i) {
+      const double a = fabs(A[i][k]);
+      const bool gt = a > amax;
+      amax = gt ? a : amax;
+      p = gt ? i : p;
+    }
+    // swap rows k and p (selects)
+#pragma unroll
+    for (int i = k + 1; i < n; ++i) {
+      const bool s = (p == i);
+#pragma unroll
+      for (int c = k; c < n; ++c) {
+        const double a = A[k][c], b = A[i][c];
+        A[k][c] = s ? b : a;
+        A[i][c] = s ? a : b;
+      }
+#pragma unroll
+      for (int c = 0; c < R; ++c) {
+        const double a = X[k][c], b = X[i][c];
+        X[k][c] = s ? b : a;
+        X[i][c] = s ? a : b;
+      }
+    }
+    const double piv = A[k][k];
+    ok = ok && (piv != 0.0);
+    const double r = 1.0 / piv;
+#pragma unroll
+    for (int i = k + 1; i < n; ++i) {
+      const double l = A[i][k] * r;
+#pragma unroll
+      for (int c = k + 1; c < n; ++c) A[i][c] = fma(-l, A[k][c], A[i][c]);
+#pragma unroll
+      for (int c = 0; c < R; ++c) X[i][c] = fma(-l, X[k][c], X[i][c]);
+    }
+  }
+  // back substitution
+#pragma unroll
+  for (int k = n - 1; k >= 0; --k) {
+    const double r = 1.0 / A[k][k];
+#pragma unroll
+    for (int c = 0; c < R; ++c) {
+      double s = X[k][c];
+#pragma unroll
+      for (int j = k + 1; j < n; ++j) s = fma(-A[k][j], X[j][c], s);
+      X[k][c] = s * r;
+    }
+  }
+  return ok;
+}
+
+// initialize_filter (filter.jl:1-10):
+//   β₀ = (I − Φ) \ δ
+//   P₀ = vec⁻¹((I − Φ⊗Φ)⁻¹ vec Q), solved on the symmetric subspace: the
+//   M(M+1)/2 unknowns P_ij (i ≤ j) of P − ΦPΦ' = Q.  That system is singular iff
+//   some λ_iλ_j = 1, exactly when the reference's M²×M² matrix is.
+// Returns false where the reference would throw (exact zero pivot).
+template <int M, int LEAD>
+__device__ __forceinline__ bool init_state(const Params<M, LEAD>& p, double (&beta)[M], double (&P)[M][M]) {
+  double A[M][M];
+  double x[M][1];
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+#pragma unroll
+    for (int j = 0; j < M; ++j) A[i][j] = (i == j ? 1.0 : 0.0) - p.Phi[i][j];
+    x[i][0] = p.delta[i];
+  }
+  bool ok = gauss_solve<M, 1>(A, x);
+#pragma unroll
+  for (int i = 0; i < M; ++i) beta[i] = x[i][0];
+
+  constexpr int S = M * (M + 1) / 2;
+  double L[S][S];
+  double q[S][1];
+  int r = 0;
+#pragma unroll
+  for (int i = 0; i < M; ++i)
+#pragma unroll
+    for (int j = i; j < M; ++j) {
+      int c = 0;
+#pragma unroll
+      for (int k = 0; k < M; ++k)
+#pragma unroll
+        for (int l = k; l < M; ++l) {
+          // coefficient of P_kl (k ≤ l) in (ΦPΦ')_ij
+          double s = p.Phi[i][k] * p.Phi[j][l];
+          if (k != l) s = fma(p.Phi[i][l], p.Phi[j][k], s);
+          L[r][c] = (r == c ? 1.0 : 0.0) - s;
+          ++c;
+        }
+      q[r][0] = p.Q[i][j];
+      ++r;
+    }
+  ok = gauss_solve<S, 1>(L, q) && ok;
+  r = 0;
+#pragma unroll
+  for (int i = 0; i < M; ++i)
+#pragma unroll
+    for (int j = i; j < M; ++j) {
+      P[i][j] = q[r][0];
+      P[j][i] = q[r][0];
+      ++r;
+    }
+  return ok;
+}
+
+// Capacitance solve.  With G = Z'Z and B̃ = σ²I + P G (= B' for B = σ²I + G P):
+//   W = B̃⁻¹ P = P B⁻¹ (symmetric),  K v = W Z'v,  P_{t|t} = σ² W,
+//   v'F⁻¹v = (v'v − u'Wu)/σ²,  det F = σ^{2(N−M)} det B̃.
+// Outputs the upper triangle of W and det B̃ (its sign is the sign of det F).
+template <int M>
+struct Capacitance {
+  __device__ __forceinline__ static void solve(const double (&P)[M][M], const double (&G)[M][M], double sigma2,
+                                               double (&W)[M][M], double& det) {
+    double A[M][M];
+    double X[M][M];
+#pragma unroll
+    for (int i = 0; i < M; ++i)
+#pragma unroll
+      for (int j = 0; j < M; ++j) {
+        double s = (i == j) ? sigma2 : 0.0;
+#pragma unroll
+        for (int l = 0; l < M; ++l) s = fma(P[i][l], G[l][j], s);
+        A[i][j] = s;
+        X[i][j] = P[i][j];
+      }
+    // LU with partial pivoting, sign tracked like LAPACK + Julia logabsdet
+    double sgn = 1.0;
+    double prod = 1.0;
+#pragma unroll
+    for (int k = 0; k < M; ++k) {
+      int p = k;
+      double amax = fabs(A[k][k]);
+#pragma unroll
+      for (int i = k + 1; i < M; ++i) {
+        const double a = fabs(A[i][k]);
+        const bool gt = a > amax;
+        amax = gt ? a : amax;
+        p = gt ? i : p;
+      }
+      sgn = (p != k) ? -sgn : sgn;
+#pragma unroll
+      for (int i = k + 1; i < M; ++i) {
+        const bool s = (p == i);
+#pragma unroll
+        for (int c = k; c < M; ++c) {
+          const double a = A[k][c], b = A[i][c];
+          A[k][c] = s ? b : a;
+          A[i][c] = s ? a : b;
+        }
+#pragma unroll
+        for (int c = 0; c < M; ++c) {
+          const double a = X[k][c], b = X[i][c];
+          X[k][c] = s ? b : a;
+          X[i][c] = s ? a : b;
+        }
+      }
+      const double piv = A[k][k];
+      prod *= piv;
+      const double r = 1.0 / piv;
+#pragma unroll
+      for (int i = k + 1; i < M; ++i) {
+        const double l = A[i][k] * r;
+#pragma unroll
+        for (int c = k + 1; c < M; ++c) A[i][c] = fma(-l, A[k][c], A[i][c]);
+#pragma unroll
+        for (int c = 0; c < M; ++c) X[i][c] = fma(-l, X[k][c], X[i][c]);
+      }
+    }
+#pragma unroll
+    for (int k = M - 1; k >= 0; --k) {
+      const double r = 1.0 / A[k][k];
+#pragma unroll
+      for (int c = 0; c < M; ++c) {
+        double s = X[k][c];
+#pragma unroll
+        for (int j = k + 1; j < M; ++j) s = fma(-A[k][j], X[j][c], s);
+        X[k][c] = s * r;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < M; ++i)
+#pragma unroll
+      for (int j = i; j < M; ++j) W[i][j] = X[i][j];
+    det = sgn * prod;
+  }
+};
+
+// M = 3: adjugate form — one reciprocal per step instead of three pivots and a
+// pivot search; det is the same cofactor expansion LAPACK's LU would sign.
+template <>
+struct Capacitance<3> {
+  __device__ __forceinline__ static void solve(const double (&P)[3][3], const double (&G)[3][3], double sigma2,
+                                               double (&W)[3][3], double& det) {
+    double a[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        double s = (i == j) ? sigma2 : 0.0;
+        s = fma(P[i][0], G[0][j], s);
+        s = fma(P[i][1], G[1][j], s);
+        s = fma(P[i][2], G[2][j], s);
+        a[i][j] = s;
+      }
+    double c[3][3];  // adj(a)
+    c[0][0] = fma(a[1][1], a[2][2], -a[1][2] * a[2][1]);
+    c[0][1] = fma(a[0][2], a[2][1], -a[0][1] * a[2][2]);
+    c[0][2] = fma(a[0][1], a[1][2], -a[0][2] * a[1][1]);
+    c[1][0] = fma(a[1][2], a[2][0], -a[1][0] * a[2][2]);
+    c[1][1] = fma(a[0][0], a[2][2], -a[0][2] * a[2][0]);
+    c[1][2] = fma(a[0][2], a[1][0], -a[0][0] * a[1][2]);
+    c[2][0] = fma(a[1][0], a[2][1], -a[1][1] * a[2][0]);
+    c[2][1] = fma(a[0][1], a[2][0], -a[0][0] * a[2][1]);
+    c[2][2] = fma(a[0][0], a[1][1], -a[0][1] * a[1][0]);
+    det = fma(a[0][0], c[0][0], fma(a[0][1], c[1][0], a[0][2] * c[2][0]));
+    const double r = 1.0 / det;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = i; j < 3; ++j) {
+        double s = c[i][0] * P[0][j];
+        s = fma(c[i][1], P[1][j], s);
+        s = fma(c[i][2], P[2][j], s);
+        W[i][j] = s * r;
+      }
+  }
+};
+
+// log|∏ d_t| accumulated as mantissa × 2^expo: one multiply and two frexp
+// instructions per step instead of a software FP64 log.
+struct LogDetAcc {
+  double mant = 1.0;
+  int expo = 0;
+  __device__ __forceinline__ void mul(double d) {
+    const double m = mant * fabs(d);
+    expo += __builtin_amdgcn_frexp_exp(m);
+    mant = __builtin_amdgcn_frexp_mant(m);
+  }
+  __device__ __forceinline__ double log_value() const { return log(mant) + (double)expo * kLn2; }
+};
+
+}  // namespace yfm

@@ -1,0 +1,115 @@
+"""Device context: one libyfm_hip context per GPU, with the panel kept resident.
+
+Replaces the reference's per-model preallocated buffers
+(``src/models/kalman/kalmanbasemodel.jl:53-69``): the panel is uploaded once and
+re-used by every objective evaluation until a different panel is passed.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+
+import numpy as np
+
+from . import _lib
+from .params import n_params, state_dim
+
+
+class Engine:
+    """Owns one ``yfm_ctx`` (include/yfm.h) on ``device``."""
+
+    def __init__(self, device: int = 0):
+        self.lib = _lib.load()
+        ctx = self.lib.yfm_create(device)
+        if not ctx:
+            raise _lib.YFMError(-2, self.lib.yfm_last_error().decode())
+        self.ctx = ctypes.c_void_p(ctx)
+        self.device = device
+        self._panel = None
+        self._mats = None
+
+    def close(self):
+        if self.ctx:
+            self.lib.yfm_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- panel -------------------------------------------------------------------
+    def set_panel(self, data, maturities, force: bool = False):
+        """data: N×T (maturities × months) like the reference's ``data`` matrix."""
+        Y = np.asfortranarray(np.asarray(data, dtype=np.float64))
+        m = np.ascontiguousarray(np.asarray(maturities, dtype=np.float64))
+        if Y.ndim != 2 or m.ndim != 1 or Y.shape[0] != m.shape[0]:
+            raise ValueError(f"panel must be N×T with N = len(maturities); got {Y.shape}, {m.shape}")
+        if (not force and self._panel is not None and self._panel.shape == Y.shape
+                and np.array_equal(self._panel, Y, equal_nan=True) and np.array_equal(self._mats, m)):
+            return
+        N, T = Y.shape
+        _lib.check(self.lib.yfm_set_panel(self.ctx, _lib.dptr(Y), N, T, _lib.dptr(m)))
+        self._panel = Y.copy(order="F")
+        self._mats = m.copy()
+
+    @property
+    def T(self):
+        return 0 if self._panel is None else self._panel.shape[1]
+
+    # ---- batched evaluation ----------------------------------------------------------
+    def loglik(self, kind: int, theta, space: int = 0, T_use=None) -> np.ndarray:
+        """Θ: P×B (or a length-P vector).  Returns B logliks (+loglik, get_loss sign)."""
+        Th = np.asarray(theta, dtype=np.float64)
+        if Th.ndim == 1:
+            Th = Th[:, None]
+        Th = np.asfortranarray(Th)
+        P, B = Th.shape
+        if P != n_params(kind):
+            raise ValueError(f"theta has {P} rows, model kind {kind} needs {n_params(kind)}")
+        out = np.empty(B, dtype=np.float64)
+        tu = None if T_use is None else np.ascontiguousarray(np.broadcast_to(T_use, (B,)), dtype=np.int32)
+        _lib.check(self.lib.yfm_loglik_batch(self.ctx, kind, space, _lib.dptr(Th), P, B, _lib.iptr(tu),
+                                             _lib.dptr(out)))
+        return out
+
+    def loglik_device(self, kind: int, d_theta: int, P: int, B: int, d_out: int, space: int = 0,
+                      d_T_use: int | None = None, stream: int | None = None) -> None:
+        """Device-pointer variant (raw addresses, e.g. ``torch.Tensor.data_ptr()``); asynchronous on ``stream``."""
+        _lib.check(self.lib.yfm_loglik_batch_device(self.ctx, kind, space, ctypes.c_void_p(d_theta), P, B,
+                                                    ctypes.c_void_p(d_T_use) if d_T_use else None,
+                                                    ctypes.c_void_p(d_out),
+                                                    ctypes.c_void_p(stream) if stream else None))
+
+    def filter_states(self, kind: int, theta, space: int = 0, T_use=None):
+        """Returns (loglik[B], beta[M, T-1, B], P[M, M, T-1, B]) — a_{t+1|t}, P_{t+1|t} after each filter! call."""
+        Th = np.asfortranarray(np.atleast_2d(np.asarray(theta, dtype=np.float64).T).T)
+        P, B = Th.shape
+        M = state_dim(kind)
+        T = self.T
+        out = np.empty(B)
+        beta = np.empty((M, max(T - 1, 0), B), order="F")
+        Pm = np.empty((M, M, max(T - 1, 0), B), order="F")
+        tu = None if T_use is None else np.ascontiguousarray(np.broadcast_to(T_use, (B,)), dtype=np.int32)
+        _lib.check(self.lib.yfm_filter_states(self.ctx, kind, space, _lib.dptr(Th), P, B, _lib.iptr(tu),
+                                              _lib.dptr(beta), _lib.dptr(Pm), _lib.dptr(out)))
+        return out, beta, Pm
+
+    def last_flags(self):
+        a, b = ctypes.c_longlong(0), ctypes.c_longlong(0)
+        _lib.check(self.lib.yfm_last_batch_flags(self.ctx, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
+
+_engines: dict[int, Engine] = {}
+_lock = threading.Lock()
+
+
+def get_engine(device: int = 0) -> Engine:
+    with _lock:
+        e = _engines.get(device)
+        if e is None:
+            e = Engine(device)
+            _engines[device] = e
+        return e
