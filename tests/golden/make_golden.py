@@ -19,6 +19,9 @@ ROOT = Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT / "yieldfactormodels.jl_amd"))
 sys.path.insert(0, str(ROOT))
 
+from concurrent.futures import ProcessPoolExecutor  # noqa: E402
+
+from oracle import kalman_mp as MP  # noqa: E402
 from oracle import kalman_oracle as O  # noqa: E402
 from yfm_amd import synthetic as S  # noqa: E402
 from yfm_amd.params import KIND_DNS, KIND_GNS, KIND_TVL, param_layout, state_dim  # noqa: E402
@@ -44,6 +47,13 @@ def run(kind, Y, mats, Th, space=0, T_use=None, n_traj=0):
     if n_traj:
         d["beta_traj"] = np.stack(trajs_b, axis=-1)  # M × (T-1) × n
         d["P_traj"] = np.stack(trajs_P, axis=-1)  # M × M × (T-1) × n
+        # 40-digit ground truth of the same recursion on the same FP64 inputs (oracle/kalman_mp.py)
+        with ProcessPoolExecutor(max_workers=min(n_traj, 6)) as ex:
+            futs = [ex.submit(MP.loglik_mp, kind, mats, Y, Th[:, b], space) for b in range(n_traj)]
+            truth = [f.result() for f in futs]
+        d["ll_truth"] = np.array([t[0] for t in truth])
+        d["beta_truth"] = np.stack([t[1] for t in truth], axis=-1)
+        d["P_truth"] = np.stack([t[2] for t in truth], axis=-1)
     return d
 
 
