@@ -1,0 +1,132 @@
+"""Extended-precision (x87 long double, 64-bit mantissa) batched truth proxy.
+
+TEST INFRASTRUCTURE ONLY (see kalman_oracle.py).  Vectorised over candidates so a
+test can adjudicate thousands of T = 600 evaluations in seconds — where the
+40-digit kalman_mp.py would take minutes per candidate.
+
+It restates get_loss (filter.jl:182-209) for the fixed-loading models in the
+CAPACITANCE form — B̃ = σ²I + P·Z'Z, pivoted Gaussian elimination — i.e. an
+algebra independent of the HIP kernel's collapsed form, carried out with ~11
+more bits than FP64, so its own error is ~κ·5e-20.  tests/test_oracle.py pins it
+to the 40-digit mpmath truth.  Initialisation follows filter.jl:1-10 (the
+M²×M² Lyapunov system, solved by pivoted elimination).  NaN columns are not
+supported here (use kalman_oracle.py / kalman_mp.py for those).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+LD = np.longdouble
+
+
+def _gesv(A, Bm):
+    """Batched Gaussian elimination with partial pivoting. A: b×n×n, Bm: b×n×r (any float dtype)."""
+    A = A.copy()
+    X = Bm.copy()
+    b, n, _ = A.shape
+    ar = np.arange(b)
+    sign = np.ones(b, dtype=A.dtype)
+    for k in range(n):
+        p = k + np.argmax(np.abs(A[:, k:, k]), axis=1)
+        sw = p != k
+        sign[sw] = -sign[sw]
+        rk = A[ar, k].copy()
+        A[ar, k] = A[ar, p]
+        A[ar, p] = rk
+        xk = X[ar, k].copy()
+        X[ar, k] = X[ar, p]
+        X[ar, p] = xk
+        for i in range(k + 1, n):
+            with np.errstate(all="ignore"):
+                l = A[:, i, k] / A[:, k, k]
+            A[:, i, k:] -= l[:, None] * A[:, k, k:]
+            X[:, i] -= l[:, None] * X[:, k]
+    for k in range(n - 1, -1, -1):
+        s = X[:, k] - np.einsum("bj,bjr->br", A[:, k, k + 1:], X[:, k + 1:])
+        with np.errstate(all="ignore"):
+            X[:, k] = s / A[:, k, k][:, None]
+    det = sign * np.prod(np.diagonal(A, axis1=1, axis2=2), axis=1)
+    return X, det
+
+
+def _transform(codes, theta):
+    th = theta.astype(LD)
+    out = th.copy()
+    with np.errstate(all="ignore"):
+        pos = codes == 1
+        out[pos] = np.exp(th[pos])
+        r = codes == 2
+        y = np.exp(th[r])
+        out[r] = 2 * y / (1 + y) - 1
+    return out
+
+
+def loglik_ld(kind: int, maturities, Y, Theta, space: int = 0) -> np.ndarray:
+    """+loglik for every column of Θ (P×B) on panel Y (N×T, no NaN); NaN where the reference throws."""
+    from .kalman_oracle import KIND_DNS, KIND_GNS, transform_codes
+    M = 3 if kind == KIND_DNS else 5
+    lead = 1 if kind == KIND_DNS else 2
+    if kind not in (KIND_DNS, KIND_GNS):
+        raise ValueError("fixed-loading kinds only")
+    codes = np.asarray(transform_codes(kind, M))
+    Theta = np.asarray(Theta, dtype=np.float64)
+    B = Theta.shape[1]
+    tc = _transform(codes[:, None].repeat(B, 1), Theta) if space == 0 else Theta.astype(LD)
+    k = lead
+    sig2 = tc[k]
+    k += 1
+    U = np.zeros((B, M, M), LD)
+    for j in range(M):
+        for i in range(j + 1):
+            U[:, i, j] = tc[k]
+            k += 1
+    Q = np.einsum("bli,blj->bij", U, U)
+    d = tc[k:k + M].T.copy()
+    k += M
+    Phi = tc[k:k + M * M].T.reshape(B, M, M).copy()
+    mats = np.asarray(maturities, dtype=np.float64).astype(LD)
+    N = len(mats)
+    Z = np.ones((B, N, M), LD)
+    for l in range(lead):
+        lam = LD(0.01) + np.exp(tc[l])
+        tau = lam[:, None] * mats[None, :]
+        z = np.exp(-tau)
+        Z[:, :, 1 + 2 * l] = (1 - z) / tau
+        Z[:, :, 2 + 2 * l] = Z[:, :, 1 + 2 * l] - z
+    G = np.einsum("bni,bnj->bij", Z, Z)
+    I = np.eye(M, dtype=LD)
+    beta, det0 = _gesv(I - Phi, d[..., None])
+    beta = beta[..., 0]
+    K2 = np.eye(M * M, dtype=LD)[None] - np.einsum("bij,bkl->bikjl", Phi, Phi).reshape(B, M * M, M * M)
+    vq = np.transpose(Q, (0, 2, 1)).reshape(B, M * M)
+    vp, det1 = _gesv(K2, vq[..., None])
+    P = np.transpose(vp[..., 0].reshape(B, M, M), (0, 2, 1))
+    throws = (det0 == 0) | (det1 == 0)
+    Y = np.asarray(Y, dtype=np.float64).astype(LD)
+    T = Y.shape[1]
+    lsum = np.zeros(B, LD)
+    qsum = np.zeros(B, LD)
+    neg = np.zeros(B, bool)
+    with np.errstate(all="ignore"):
+        for t in range(T - 1):
+            y = Y[:, t]
+            zy = np.einsum("bni,n->bi", Z, y)
+            u = zy - np.einsum("bij,bj->bi", G, beta)
+            r = y[None, :] - np.einsum("bni,bi->bn", Z, beta)
+            vv = np.einsum("bn,bn->b", r, r)
+            Bt = sig2[:, None, None] * I + P @ G
+            W, det = _gesv(Bt, P)
+            W = (W + np.transpose(W, (0, 2, 1))) / 2
+            kv = np.einsum("bij,bj->bi", W, u)
+            q = (vv - np.einsum("bi,bi->b", u, kv)) / sig2
+            beta = d + np.einsum("bij,bj->bi", Phi, beta + kv)
+            P = sig2[:, None, None] * (Phi @ W @ np.transpose(Phi, (0, 2, 1))) + Q
+            if t >= 1:
+                lsum += np.log(np.abs(det))
+                qsum += q
+                neg |= det < 0
+        const = (N - M) * np.log(sig2) + N * np.log(2 * LD(np.pi))
+        ll = (-((T - 2) * const + lsum + qsum) / 2).astype(np.float64)
+    ll[neg | ~np.isfinite(ll)] = -np.inf
+    ll[throws] = np.nan
+    return ll

@@ -106,6 +106,19 @@ def main():
     Tht[:, 0] = S.theta0(KIND_TVL)
     fixtures["tvl_basic"] = run(KIND_TVL, Yt, m40, Tht, n_traj=1)
 
+    # 8. Headline shape (T = 600, N = 30): four columns of the bench batch on which the
+    #    reference's own dense FP64 arithmetic is far (up to 5e-6) from exact arithmetic,
+    #    plus two benign ones; ll_truth is the 40-digit value (oracle/kalman_mp.py).
+    Y600 = S.simulate_panel(KIND_DNS, 600)
+    idx = [10283, 1679, 5390, 22413, 0, 1]
+    Thh = np.asfortranarray(S.theta_batch(KIND_DNS, 65536)[:, idx])
+    d = run(KIND_DNS, Y600, mats30, Thh)
+    with ProcessPoolExecutor(max_workers=6) as ex:
+        futs = [ex.submit(MP.loglik_mp, KIND_DNS, mats30, Y600, Thh[:, b], 0) for b in range(len(idx))]
+        d["ll_truth"] = np.array([f.result()[0] for f in futs])
+    d["bench_index"] = np.asarray(idx)
+    fixtures["dns_hard_T600"] = d
+
     for name, d in fixtures.items():
         np.savez_compressed(OUT / f"{name}.npz", **d)
         print(name, d["loglik"])

@@ -114,12 +114,33 @@ def test_golden_numpy_oracle_reproduces(name):
 
 @pytest.mark.parametrize("name", GOLDEN_NAMES)
 def test_golden_c_oracle_agrees(name, coracle):
-    """Independent C restatement (own getrf/getri) vs the NumPy/LAPACK fixtures."""
+    """Independent C restatement (own getrf/getri) vs the NumPy/LAPACK fixtures.
+
+    dns_hard_T600 holds candidates on which the reference's dense FP64 arithmetic is
+    itself 1e-7..1e-5 away from exact arithmetic: there both restatements are checked
+    against the 40-digit truth instead (and must land within that band)."""
     g = load_golden(name)
     kind = int(g["kind"])
     out = coracle(kind, g["Y"], g["maturities"], g["Theta"], space=int(g["space"]), T_use=g.get("T_use"))
+    if name == "dns_hard_T600":
+        assert rel_err(out, g["ll_truth"]) <= 1e-5
+        assert rel_err(g["loglik"], g["ll_truth"]) <= 1e-5
+        return
     tol = 2e-9 if kind == KIND_TVL else 1e-9  # north-star tolerance; observed ≤ 2e-10
     assert rel_err(out, g["loglik"]) <= tol
+
+
+@pytest.mark.parametrize("name", [n for n in GOLDEN_NAMES if "ll_truth" in load_golden(n)])
+def test_long_double_proxy_pinned_to_mp_truth(name):
+    """oracle/kalman_ld.py (extended precision, capacitance algebra) vs the 40-digit truth."""
+    from oracle.kalman_ld import loglik_ld
+    g = load_golden(name)
+    kind = int(g["kind"])
+    if kind == KIND_TVL or np.isnan(g["Y"]).any():
+        pytest.skip("kalman_ld covers fixed-loading kinds on NaN-free panels")
+    k = len(g["ll_truth"])
+    got = loglik_ld(kind, g["maturities"], g["Y"], g["Theta"][:, :k], space=int(g["space"]))
+    assert rel_err(got, g["ll_truth"]) <= 1e-11
 
 
 def test_c_oracle_headline_batch(coracle):

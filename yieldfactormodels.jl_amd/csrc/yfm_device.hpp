@@ -279,46 +279,65 @@ struct Capacitance {
   }
 };
 
-// M = 3: adjugate form — one reciprocal per step instead of three pivots and a
-// pivot search; det is the same cofactor expansion LAPACK's LU would sign.
-template <>
-struct Capacitance<3> {
-  __device__ __forceinline__ static void solve(const double (&P)[3][3], const double (&G)[3][3], double sigma2,
-                                               double (&W)[3][3], double& det) {
-    double a[3][3];
+// 1/d to ~1 ulp: v_rcp_f64 plus two Newton steps (no IEEE special-casing needed:
+// a zero or non-finite d yields a non-finite result, which the callers treat
+// exactly like the reference's singular / non-finite cases).
+__device__ __forceinline__ double rcp_nr(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = fma(-d, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-d, r, 1.0);
+  return fma(r, e, r);
+}
+
+// Symmetric LDLᵀ (no pivoting) of an M×M matrix S, solving S X = Rhs in place for
+// R right-hand sides; returns det S = ∏ d_i (its sign is exact in the factorised
+// arithmetic).  Used on S = P + σ²(Z'Z)⁻¹, which is SPD whenever P is PSD.
+template <int M, int R>
+__device__ __forceinline__ double ldlt_solve(const double (&S)[M][M], double (&X)[M][R]) {
+  double L[M][M];  // strictly lower part used
+  double a[M][M];  // a[i][k] = L[i][k] * d[k]
+  double d[M], rd[M];
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
+  for (int j = 0; j < M; ++j) {
+    double dj = S[j][j];
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        double s = (i == j) ? sigma2 : 0.0;
-        s = fma(P[i][0], G[0][j], s);
-        s = fma(P[i][1], G[1][j], s);
-        s = fma(P[i][2], G[2][j], s);
-        a[i][j] = s;
-      }
-    double c[3][3];  // adj(a)
-    c[0][0] = fma(a[1][1], a[2][2], -a[1][2] * a[2][1]);
-    c[0][1] = fma(a[0][2], a[2][1], -a[0][1] * a[2][2]);
-    c[0][2] = fma(a[0][1], a[1][2], -a[0][2] * a[1][1]);
-    c[1][0] = fma(a[1][2], a[2][0], -a[1][0] * a[2][2]);
-    c[1][1] = fma(a[0][0], a[2][2], -a[0][2] * a[2][0]);
-    c[1][2] = fma(a[0][2], a[1][0], -a[0][0] * a[1][2]);
-    c[2][0] = fma(a[1][0], a[2][1], -a[1][1] * a[2][0]);
-    c[2][1] = fma(a[0][1], a[2][0], -a[0][0] * a[2][1]);
-    c[2][2] = fma(a[0][0], a[1][1], -a[0][1] * a[1][0]);
-    det = fma(a[0][0], c[0][0], fma(a[0][1], c[1][0], a[0][2] * c[2][0]));
-    const double r = 1.0 / det;
+    for (int k = 0; k < j; ++k) dj = fma(-a[j][k], L[j][k], dj);
+    d[j] = dj;
+    rd[j] = rcp_nr(dj);
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
+    for (int i = j + 1; i < M; ++i) {
+      double s = S[i][j];
 #pragma unroll
-      for (int j = i; j < 3; ++j) {
-        double s = c[i][0] * P[0][j];
-        s = fma(c[i][1], P[1][j], s);
-        s = fma(c[i][2], P[2][j], s);
-        W[i][j] = s * r;
-      }
+      for (int k = 0; k < j; ++k) s = fma(-a[i][k], L[j][k], s);
+      a[i][j] = s;
+      L[i][j] = s * rd[j];
+    }
   }
-};
+#pragma unroll
+  for (int c = 0; c < R; ++c) {
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      double s = X[i][c];
+#pragma unroll
+      for (int k = 0; k < i; ++k) s = fma(-L[i][k], X[k][c], s);
+      X[i][c] = s;
+    }
+#pragma unroll
+    for (int i = 0; i < M; ++i) X[i][c] *= rd[i];
+#pragma unroll
+    for (int i = M - 1; i >= 0; --i) {
+      double s = X[i][c];
+#pragma unroll
+      for (int k = i + 1; k < M; ++k) s = fma(-L[k][i], X[k][c], s);
+      X[i][c] = s;
+    }
+  }
+  double det = d[0];
+#pragma unroll
+  for (int i = 1; i < M; ++i) det *= d[i];
+  return det;
+}
 
 // log|∏ d_t| accumulated as mantissa × 2^expo: one multiply and two frexp
 // instructions per step instead of a software FP64 log.

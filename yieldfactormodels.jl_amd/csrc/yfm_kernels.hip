@@ -9,12 +9,24 @@
 // columns) live in VGPRs.  All lanes walk the same time index t, so the panel
 // column y_t is wave-uniform: the workgroup stages TC columns at a time into LDS
 // (one coalesced global sweep per chunk, prefetched into registers one chunk ahead)
-// and every lane reads them as LDS broadcasts.  Nothing N×N is ever formed: the
-// per-step solve runs on the M×M capacitance matrix B̃ = σ²I + P·Z'Z.
+// and every lane reads them as LDS broadcasts.  Nothing N×N is ever formed.
+//
+// Per-step algebra — the COLLAPSED form: with G = Z'Z, R = σ²G⁻¹,
+// ĉ_t = G⁻¹Z'y_t (cross-sectional OLS factors), r'r_t = ‖y_t − Zĉ_t‖²,
+// c = ĉ_t − β and S = P + R (M×M, symmetric):
+//     v'F⁻¹v = r'r/σ² + c'S⁻¹c,        log det F = (N−M) log σ² + log det G + log det S,
+//     β_{t|t} = β + P S⁻¹ c,            P_{t|t}  = P S⁻¹ R,
+// all exact rewrites of filter.jl:143-176 (F = ZPZ' + σ²I, K = PZ'F⁻¹, I − KZ).
+// r'r is formed from CENTERED columns ỹ = y − ȳ1 (1 = Z e₁ for every candidate),
+// which removes the y'y − ŷ'ŷ cancellation.  S is factorised by LDLᵀ.
+// Lanes whose Z'Z is numerically singular (N < M, or λ so large that Z's columns
+// collapse) take the CAPACITANCE form instead: B̃ = σ²I + PG, pivoted LU,
+// W = B̃⁻¹P, v'F⁻¹v = (v'v − u'Wu)/σ², P_{t|t} = σ²W, log det F = (N−M) log σ² +
+// log det B̃.
 //
 // Panel layout in HBM (built by prep_panel_kernel from the caller's N×T
 // column-major matrix): T columns of LDP = NP + 4 doubles —
-//   [ y_0 … y_{N-1}, 0 … 0 (to NP), S1 = Σy, YY = Σy², isnan(any y), 0 ].
+//   [ ỹ_0 … ỹ_{N-1}, 0 … 0 (to NP), ȳ, ỹ'ỹ, isnan(any y), y'y ].
 #include "yfm_device.hpp"
 
 namespace yfm {
@@ -35,19 +47,25 @@ __global__ void prep_panel_kernel(const double* __restrict__ Y, int N, int T, in
     nan = nan || (v != v);
     s1 += v;
     yy = fma(v, v, yy);
-    o[i] = v;
+  }
+  const double ybar = s1 / (double)N;
+  double tt = 0.0;
+  for (int i = 0; i < N; ++i) {
+    const double d = y[i] - ybar;
+    o[i] = d;
+    tt = fma(d, d, tt);
   }
   for (int i = N; i < np; ++i) o[i] = 0.0;
-  o[np] = s1;
-  o[np + 1] = yy;
+  o[np] = ybar;
+  o[np + 1] = tt;
   o[np + 2] = nan ? 1.0 : 0.0;
-  o[np + 3] = 0.0;
+  o[np + 3] = yy;
 }
 
 // Fixed-loading models: DNS (M = 3, one γ, dns.jl:51-65) and the 5-factor
 // generalised NS extension (M = 5, two γ; SURVEY §8 a9, not in the reference).
-// Z column 0 is ones (its Z'y is the precomputed S1); columns 1.. come in
-// (slope, curvature) pairs per γ: S = (1 − e^{−λm})/(λm), C = S − e^{−λm}.
+// Z column 0 is ones; columns 1.. come in (slope, curvature) pairs per γ:
+// S = (1 − e^{−λm})/(λm), C = S − e^{−λm}.
 template <int NP, int M, int LEAD, bool RECORD>
 __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     const double* __restrict__ theta, int P, int B, int space, const double* __restrict__ panel, int T, int N,
@@ -111,11 +129,42 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
       G[d + 1][c + 1] = g;
     }
   }
+  const double sigma2 = p.sigma2;
+  const double rsig2 = 1.0 / sigma2;
+
+  // G⁻¹ (pivoted elimination) and log det G; decide collapsed vs capacitance per lane.
+  double R[M][M];
+  double logdetG = 0.0;
+  bool collapsed;
+  {
+    double A[M][M], X[M][M];
+    double hadamard = 1.0;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      hadamard *= G[i][i];
+#pragma unroll
+      for (int j = 0; j < M; ++j) {
+        A[i][j] = G[i][j];
+        X[i][j] = (i == j) ? 1.0 : 0.0;
+      }
+    }
+    const bool ok = gauss_solve<M, M>(A, X);
+    double detG = 1.0;
+#pragma unroll
+    for (int i = 0; i < M; ++i) detG *= A[i][i];
+    detG = fabs(detG);
+    // Z'Z must be numerically nonsingular: det / ∏ diag (Hadamard ratio, ≤ 1).
+    collapsed = ok && (N >= M) && (detG > 1e-13 * hadamard);
+    logdetG = collapsed ? log(detG) : 0.0;
+#pragma unroll
+    for (int i = 0; i < M; ++i)
+#pragma unroll
+      for (int j = 0; j < M; ++j) R[i][j] = sigma2 * 0.5 * (X[i][j] + X[j][i]);
+  }
+  // Gi·(0, z̃) only needs the columns 1.. of G⁻¹ = R/σ²
 
   double beta[M], Pm[M][M];
   const bool init_ok = init_state<M, LEAD>(p, beta, Pm);
-  const double sigma2 = p.sigma2;
-  const double rsig2 = 1.0 / sigma2;
 
   LogDetAcc ld;
   double sumq = 0.0;
@@ -154,12 +203,12 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     for (int tt = 0; tt < tend; ++tt) {
       const int t = c * kTC + tt;  // 0-based step; reads column t (Julia t+1)
       const double* col = buf + tt * LDP;
-      const double nanflag = col[NP + 2];
+      const double2 meta = *reinterpret_cast<const double2*>(col + NP + 2);  // (nanflag, y'y)
       const bool act = t < my_steps;
       if (!act) continue;
       const bool acc = t >= 1;  // Julia t > 1 (filter.jl:194)
 
-      if (nanflag != 0.0) {
+      if (meta.x != 0.0) {
         // NaN column: prediction only (filter.jl:126-140); F, v stale → the loglik
         // re-adds the previous term (filter.jl:195 reads base.F / base.v unchanged).
         double nb[M];
@@ -198,10 +247,9 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
           neg = neg || (last_det < 0.0);
         }
       } else {
-        // ---- Z'y_t: column 0 is S1, the others are dot products with y_t ----
-        const double2 sy = *reinterpret_cast<const double2*>(col + NP);  // (S1, YY)
-        double zy[M];
-        zy[0] = sy.x;
+        // ---- z̃ = Z'ỹ_t for the non-constant columns (Σỹ = 0) ----
+        const double2 yb = *reinterpret_cast<const double2*>(col + NP);  // (ȳ, ỹ'ỹ)
+        double zt[NZ];
         {
           double a[NZ][2];
 #pragma unroll
@@ -216,55 +264,108 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
             }
           }
 #pragma unroll
-          for (int cz = 0; cz < NZ; ++cz) zy[cz + 1] = a[cz][0] + a[cz][1];
+          for (int cz = 0; cz < NZ; ++cz) zt[cz] = a[cz][0] + a[cz][1];
         }
-        const double yy = sy.y;
-        // u = Z'v = Z'y − Gβ ;  v'v = y'y − 2β'Z'y + β'Gβ
-        double u[M];
-        double bgb = 0.0, bzy = 0.0;
+        double det, q;
+        double bf[M];   // β_{t|t}
+        double Pf[M][M];  // P_{t|t}
+        if (collapsed) {
+          // ĉ = G⁻¹ (0, z̃) + ȳ e₀ ;  r'r = ỹ'ỹ − z̃'ĉ[1:]
+          double ch[M];
 #pragma unroll
-        for (int i = 0; i < M; ++i) {
-          double g = 0.0;
+          for (int i = 0; i < M; ++i) {
+            double s = 0.0;
 #pragma unroll
-          for (int j = 0; j < M; ++j) g = fma(G[i][j], beta[j], g);
-          u[i] = zy[i] - g;
-          bgb = fma(beta[i], g, bgb);
-          bzy = fma(beta[i], zy[i], bzy);
+            for (int j = 1; j < M; ++j) s = fma(R[i][j], zt[j - 1], s);
+            ch[i] = s * rsig2;
+          }
+          double rr = yb.y;
+#pragma unroll
+          for (int j = 1; j < M; ++j) rr = fma(-zt[j - 1], ch[j], rr);
+          ch[0] += yb.x;
+          double S[M][M];
+          double X[M][M + 1];  // [c | R] → [S⁻¹c | S⁻¹R]
+#pragma unroll
+          for (int i = 0; i < M; ++i) {
+#pragma unroll
+            for (int j = 0; j < M; ++j) {
+              S[i][j] = Pm[i][j] + R[i][j];
+              X[i][j + 1] = R[i][j];
+            }
+            X[i][0] = ch[i] - beta[i];
+          }
+          det = ldlt_solve<M, M + 1>(S, X);
+          double cx = 0.0;
+#pragma unroll
+          for (int i = 0; i < M; ++i) cx = fma(ch[i] - beta[i], X[i][0], cx);
+          q = fma(rr, rsig2, cx);
+#pragma unroll
+          for (int i = 0; i < M; ++i) {
+            double s = beta[i];
+#pragma unroll
+            for (int k = 0; k < M; ++k) s = fma(Pm[i][k], X[k][0], s);
+            bf[i] = s;
+          }
+#pragma unroll
+          for (int i = 0; i < M; ++i)
+#pragma unroll
+            for (int j = i; j < M; ++j) {
+              double s = 0.0;
+#pragma unroll
+              for (int k = 0; k < M; ++k) s = fma(Pm[i][k], X[k][j + 1], s);
+              Pf[i][j] = s;
+              Pf[j][i] = s;
+            }
+        } else {
+          // capacitance form on uncentered sums: Z'y = (Nȳ, z̃ + ȳ G[1:,0]), y'y
+          double zy[M];
+          zy[0] = (double)N * yb.x;
+#pragma unroll
+          for (int j = 1; j < M; ++j) zy[j] = fma(yb.x, G[j][0], zt[j - 1]);
+          double u[M];
+          double bgb = 0.0, bzy = 0.0;
+#pragma unroll
+          for (int i = 0; i < M; ++i) {
+            double g = 0.0;
+#pragma unroll
+            for (int j = 0; j < M; ++j) g = fma(G[i][j], beta[j], g);
+            u[i] = zy[i] - g;
+            bgb = fma(beta[i], g, bgb);
+            bzy = fma(beta[i], zy[i], bzy);
+          }
+          const double vv = fma(-2.0, bzy, meta.y) + bgb;
+          double W[M][M];
+          Capacitance<M>::solve(Pm, G, sigma2, W, det);
+#pragma unroll
+          for (int i = 0; i < M; ++i)
+#pragma unroll
+            for (int j = 0; j < i; ++j) W[i][j] = W[j][i];
+          double uk = 0.0;
+#pragma unroll
+          for (int i = 0; i < M; ++i) {
+            double s = 0.0;
+#pragma unroll
+            for (int j = 0; j < M; ++j) s = fma(W[i][j], u[j], s);
+            bf[i] = beta[i] + s;
+            uk = fma(u[i], s, uk);
+          }
+          q = (vv - uk) * rsig2;
+#pragma unroll
+          for (int i = 0; i < M; ++i)
+#pragma unroll
+            for (int j = 0; j < M; ++j) Pf[i][j] = sigma2 * W[i][j];
         }
-        const double vv = fma(-2.0, bzy, yy) + bgb;
-
-        double W[M][M];
-        double det;
-        Capacitance<M>::solve(Pm, G, sigma2, W, det);
-#pragma unroll
-        for (int i = 0; i < M; ++i)
-#pragma unroll
-          for (int j = 0; j < i; ++j) W[i][j] = W[j][i];
 
         const bool upd = !(t == 0 && det == 0.0);  // inv(F) threw at t=1: skip update (filter.jl:151-154)
-        double kv[M];
-        double uk = 0.0;
-#pragma unroll
-        for (int i = 0; i < M; ++i) {
-          double s = 0.0;
-#pragma unroll
-          for (int j = 0; j < M; ++j) s = fma(W[i][j], u[j], s);
-          kv[i] = s;
-          uk = fma(u[i], s, uk);
-        }
-        const double q = (vv - uk) * rsig2;
         if (upd) {
-          double bf[M];
 #pragma unroll
-          for (int i = 0; i < M; ++i) bf[i] = beta[i] + kv[i];  // filter.jl:162
-#pragma unroll
-          for (int i = 0; i < M; ++i) {  // filter.jl:163-165
+          for (int i = 0; i < M; ++i) {  // β ← δ + Φ β_{t|t}   (filter.jl:162-165)
             double s = p.delta[i];
 #pragma unroll
             for (int j = 0; j < M; ++j) s = fma(p.Phi[i][j], bf[j], s);
             beta[i] = s;
           }
-          // P ← Φ (σ² W) Φ' + Q   (≡ Φ(I − KZ)PΦ' + Q, filter.jl:168-176)
+          // P ← Φ P_{t|t} Φ' + Q   (≡ Φ(I − KZ)PΦ' + Q, filter.jl:168-176)
           double A[M][M];
 #pragma unroll
           for (int i = 0; i < M; ++i)
@@ -272,17 +373,16 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
             for (int j = 0; j < M; ++j) {
               double s = 0.0;
 #pragma unroll
-              for (int l = 0; l < M; ++l) s = fma(p.Phi[i][l], W[l][j], s);
+              for (int l = 0; l < M; ++l) s = fma(p.Phi[i][l], Pf[l][j], s);
               A[i][j] = s;
             }
 #pragma unroll
           for (int i = 0; i < M; ++i)
 #pragma unroll
             for (int j = i; j < M; ++j) {
-              double s = 0.0;
+              double s = p.Q[i][j];
 #pragma unroll
               for (int l = 0; l < M; ++l) s = fma(A[i][l], p.Phi[j][l], s);
-              s = fma(sigma2, s, p.Q[i][j]);
               Pm[i][j] = s;
               Pm[j][i] = s;
             }
@@ -319,7 +419,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     if (nterms == 0) {
       ll = 0.0;
     } else {
-      const double per_term = (double)(N - M) * log(sigma2) + (double)N * kLog2Pi;
+      const double per_term = (double)(N - M) * log(sigma2) + logdetG + (double)N * kLog2Pi;
       ll = -0.5 * ((double)nterms * per_term + ld.log_value() + sumq);
     }
     if (neg || !isfinite(ll)) {  // DomainError / non-finite → -Inf (filter.jl:197-204)
