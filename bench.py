@@ -84,6 +84,18 @@ def cpu_baseline(Y, mats, Th, seconds: float, gpu_out):
                        "oracle_vs_truth_max_rel": float(e_ref.max()) if e_ref.size else 0.0}}
 
 
+def pmc_traffic(kernel_substr: str = "fixedz_loglik_kernel<32, 3, 1, false>"):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 --pmc passes
+    (tools/profile_pmc.sh → profiles/<round>/pmc_summary.json): (FETCH_SIZE + WRITE_SIZE) KB × 1024, raw
+    (gfx950 FETCH_SIZE can under-count narrow reads by up to 2×, MI355X_MICROARCH.md §HBM)."""
+    for rnd in sorted((ROOT / "profiles").glob("r*/pmc_summary.json"), reverse=True):
+        d = json.loads(rnd.read_text())
+        for k, v in d.items():
+            if kernel_substr in k and "FETCH_SIZE" in v and "WRITE_SIZE" in v:
+                return (v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024.0, str(rnd.relative_to(ROOT))
+    return None, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -148,6 +160,7 @@ def main():
     value = world * B / (wall / args.steps)
     f_eval = alg_flops(kind, N, M, T)
     achieved = f_eval * B / (ev_ms * 1e-3) / 1e12  # TFLOP/s of the dominant kernel (per GPU)
+    traffic, traffic_src = pmc_traffic()
     out_host = d_out.cpu().numpy()
     n_neginf, n_nan = int(np.isneginf(out_host).sum()), int(np.isnan(out_host).sum())
 
@@ -173,7 +186,9 @@ def main():
                        "N": N, "batch_per_gpu": B, "global_batch": world * B,
                        "parallelism": f"dp{world} (θ sharded, RCCL all-gather of logliks + argmax)"},
             "roofline": {"bound": "fp64-valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
+                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
+                         "traffic_source": traffic_src,
+                         "algorithmic_bytes": B * (P + 1) * 8 + T * (32 + 4) * 8,
                          "kernel_ms": ev_ms, "flops_per_eval": f_eval,
                          "note": "achieved = SURVEY §8d algorithmic flops × B ÷ HIP-event time per step"},
             "cpu_baseline": cpu,
