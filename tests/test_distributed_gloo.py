@@ -1,0 +1,75 @@
+"""Multi-process (world_size 2, gloo, CPU) tests of the sharding / gather / argmax logic.
+
+The per-rank compute here is the NumPy oracle (test infrastructure); on GPUs the
+same code runs with the HIP library per rank and the nccl (RCCL) backend (bench.py)."""
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from yfm_amd import distributed as D
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_shard_range_partitions():
+    for n in (0, 1, 7, 64, 65536, 65537):
+        for w in (1, 2, 3, 8):
+            parts = [D.shard_range(n, w, r) for r in range(w)]
+            assert parts[0][0] == 0 and parts[-1][1] == n
+            assert all(parts[i][1] == parts[i + 1][0] for i in range(w - 1))
+            sizes = [h - l for l, h in parts]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_window_shards_cover_and_balance():
+    counts = [5, 8, 3, 4096]
+    for w in (2, 3, 8):
+        allidx = np.sort(np.concatenate([D.window_shards(counts, w, r) for r in range(w)]))
+        np.testing.assert_array_equal(allidx, np.arange(sum(counts)))
+        per = [len(D.window_shards(counts, w, r)) for r in range(w)]
+        assert max(per) - min(per) <= len(counts)
+
+
+def _worker(rank, world, port, Theta, Y, mats, ret):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import kalman_oracle as O
+
+    def evaluate(Th):
+        return torch.tensor([O.loglik(0, mats, 3, Y, Th[:, b]) for b in range(Th.shape[1])], dtype=torch.float64)
+
+    res = D.sharded_loglik(Theta, evaluate)
+    if rank == 0:
+        ret["ll"] = res.loglik.numpy()
+        ret["best"] = (res.best_index, res.best_value)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_sharded_equals_single_process(world):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+    from oracle import kalman_oracle as O
+    from yfm_amd import synthetic as S
+    Y = S.simulate_panel(0, 40)
+    mats = S.maturities_30()
+    Theta = S.theta_batch(0, 7, seed=3, bad_frac=0.0)
+    Theta[:, 4] = S.theta0(0)
+    ref = np.array([O.loglik(0, mats, 3, Y, Theta[:, b]) for b in range(7)])
+    mgr = mp.Manager()
+    ret = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), Theta, Y, mats, ret), nprocs=world, join=True)
+    np.testing.assert_array_equal(ret["ll"], ref)
+    assert ret["best"][0] == int(np.argmax(ref)) and ret["best"][1] == ref.max()

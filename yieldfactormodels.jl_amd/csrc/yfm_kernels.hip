@@ -62,10 +62,136 @@ __global__ void prep_panel_kernel(const double* __restrict__ Y, int N, int T, in
   o[np + 3] = yy;
 }
 
+// ---- per-step building blocks (all __forceinline__: the fast path is one basic block) ----
+
+// z̃ = Z'ỹ_t for the NZ non-constant loading columns (Σỹ = 0 removes column 0).
+template <int NP, int NZ>
+__device__ __forceinline__ void dot_zt(const double* __restrict__ col, const double (&Zc)[NZ][NP], double (&zt)[NZ]) {
+  double a[NZ][2];
+#pragma unroll
+  for (int cz = 0; cz < NZ; ++cz) {
+    a[cz][0] = 0.0;
+    a[cz][1] = 0.0;
+  }
+#pragma unroll
+  for (int i = 0; i < NP; i += 2) {
+    const double2 y2 = *reinterpret_cast<const double2*>(col + i);
+#pragma unroll
+    for (int cz = 0; cz < NZ; ++cz) {
+      a[cz][0] = fma(Zc[cz][i], y2.x, a[cz][0]);
+      a[cz][1] = fma(Zc[cz][i + 1], y2.y, a[cz][1]);
+    }
+  }
+#pragma unroll
+  for (int cz = 0; cz < NZ; ++cz) zt[cz] = a[cz][0] + a[cz][1];
+}
+
+// Collapsed-form measurement update (see the header): returns det S and q = v'F⁻¹v,
+// writes β_{t|t} (bf) and the upper triangle of P_{t|t} (Pf).
+template <int M>
+__device__ __forceinline__ void collapsed_update(const double (&zt)[M - 1], double ybar, double ytt,
+                                                 const double (&R)[M][M], double rsig2, const double (&beta)[M],
+                                                 const double (&Pm)[M][M], double (&bf)[M], double (&Pf)[M][M],
+                                                 double& det, double& q) {
+  double zs[M - 1];
+#pragma unroll
+  for (int j = 0; j < M - 1; ++j) zs[j] = zt[j] * rsig2;
+  double ch[M];  // ĉ = G⁻¹(0, z̃) (= R/σ² · (0, z̃))
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    double s = 0.0;
+#pragma unroll
+    for (int j = 1; j < M; ++j) s = fma(R[i][j], zs[j - 1], s);
+    ch[i] = s;
+  }
+  double rr = ytt;  // ‖ỹ − Zĉ‖² = ỹ'ỹ − z̃'ĉ
+#pragma unroll
+  for (int j = 1; j < M; ++j) rr = fma(-zt[j - 1], ch[j], rr);
+  ch[0] += ybar;
+  double S[M][M];
+  double X[M][M + 1];  // [c | R] → [S⁻¹c | S⁻¹R]
+  double c[M];
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    c[i] = ch[i] - beta[i];
+#pragma unroll
+    for (int j = 0; j <= i; ++j) S[i][j] = Pm[i][j] + R[i][j];  // LDLᵀ reads the lower triangle only
+#pragma unroll
+    for (int j = 0; j < M; ++j) X[i][j + 1] = R[i][j];
+    X[i][0] = c[i];
+  }
+  det = ldlt_solve<M, M + 1>(S, X);
+  double cx = 0.0;
+#pragma unroll
+  for (int i = 0; i < M; ++i) cx = fma(c[i], X[i][0], cx);
+  q = fma(rr, rsig2, cx);
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    double s = beta[i];
+#pragma unroll
+    for (int k = 0; k < M; ++k) s = fma(Pm[i][k], X[k][0], s);
+    bf[i] = s;
+  }
+#pragma unroll
+  for (int i = 0; i < M; ++i)
+#pragma unroll
+    for (int j = i; j < M; ++j) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < M; ++k) s = fma(Pm[i][k], X[k][j + 1], s);
+      Pf[i][j] = s;
+    }
+}
+
+// β ← δ + Φ β_{t|t};  P ← Φ P_{t|t} Φ' + Q   (filter.jl:162-176).  Pf: upper triangle.
+template <int M, int LEAD>
+__device__ __forceinline__ void propagate(const Params<M, LEAD>& p, const double (&bf)[M], const double (&Pf)[M][M],
+                                          double (&beta)[M], double (&Pm)[M][M]) {
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    double s = p.delta[i];
+#pragma unroll
+    for (int j = 0; j < M; ++j) s = fma(p.Phi[i][j], bf[j], s);
+    beta[i] = s;
+  }
+  double A[M][M];
+#pragma unroll
+  for (int i = 0; i < M; ++i)
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      double s = 0.0;
+#pragma unroll
+      for (int l = 0; l < M; ++l) s = fma(p.Phi[i][l], (l <= j) ? Pf[l][j] : Pf[j][l], s);
+      A[i][j] = s;
+    }
+#pragma unroll
+  for (int i = 0; i < M; ++i)
+#pragma unroll
+    for (int j = i; j < M; ++j) {
+      double s = p.Q[i][j];
+#pragma unroll
+      for (int l = 0; l < M; ++l) s = fma(A[i][l], p.Phi[j][l], s);
+      Pm[i][j] = s;
+      Pm[j][i] = s;
+    }
+}
+
+typedef double yfm_double4 __attribute__((ext_vector_type(4)));
+
 // Fixed-loading models: DNS (M = 3, one γ, dns.jl:51-65) and the 5-factor
 // generalised NS extension (M = 5, two γ; SURVEY §8 a9, not in the reference).
 // Z column 0 is ones; columns 1.. come in (slope, curvature) pairs per γ:
 // S = (1 − e^{−λm})/(λm), C = S − e^{−λm}.
+//
+// Z'ỹ_t for a whole wave is a GEMM: [64 candidates × NZ loading columns] × [NP
+// maturities] · [NP × 16 steps].  With MFMA (NZ = 2, DNS) each wave computes it for
+// 16 steps at a time with v_mfma_f64_16x16x4_f64 — A = the wave's loadings (held in
+// registers as MFMA fragments for the whole filter), B = the staged panel columns —
+// and hands each lane its own (z̃₀, z̃₁) through a per-wave LDS scratch.  The VALU
+// then runs only the M×M update.  Without MFMA (GNS5) the dot products are VALU FMAs
+// computed one step ahead, inside the same basic block as the update.
+// A wave-uniform fast path (no NaN column, every lane active, every lane collapsed,
+// t ≥ 1) carries no per-lane masking; everything else takes the general path.
 template <int NP, int M, int LEAD, bool RECORD>
 __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     const double* __restrict__ theta, int P, int B, int space, const double* __restrict__ panel, int T, int N,
@@ -75,11 +201,22 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   constexpr int CH = kTC * LDP;               // doubles per chunk
   constexpr int PER = (CH + kBlock - 1) / kBlock;
   constexpr int NZ = M - 1;                   // non-constant loading columns
+  constexpr bool USE_MFMA = (NZ == 2);
+  constexpr int NK = (NP + 3) / 4;            // MFMA k-steps (4 maturities each)
+  constexpr int NRT = 64 * NZ / 16;           // MFMA row tiles per wave (16 (cand, col) pairs each)
+  constexpr int TB = 16;                      // steps per MFMA block
+  constexpr int SS = 64 * NZ + 2;             // scratch row stride (doubles): one row per step
+  constexpr int SCR = USE_MFMA ? (TB * SS) : 2;
   static_assert(NZ == 2 * LEAD, "loading columns come in (S, C) pairs per gamma");
+  static_assert(NP % 2 == 0, "double2 panel reads");
+  static_assert(kTC % TB == 0, "MFMA blocks tile the panel chunk");
   __shared__ __attribute__((aligned(16))) double sh[2][CH];
+  __shared__ __attribute__((aligned(16))) double scratch[kBlock / 64][SCR];
   __shared__ int s_nobs_max;
 
   const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
   const int b = blockIdx.x * kBlock + tid;
   const bool live = b < B;
   const int bb = live ? b : (B - 1);
@@ -129,6 +266,36 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
       G[d + 1][c + 1] = g;
     }
   }
+
+  // MFMA A fragments: tile r, k-step kk — lane l holds Z of pair p = 16r + (l & 15)
+  // (candidate p >> 1 of this wave, column p & 1) at maturity 4kk + (l >> 4).
+  // Gathered once through the wave's scratch, 16 candidates at a time.
+  double Af[USE_MFMA ? NRT : 1][USE_MFMA ? NK : 1];
+  if constexpr (USE_MFMA) {
+    constexpr int ZS = 4 * NK;  // padded maturity stride of the staging image
+    constexpr int QT = NRT / 4;  // row tiles per quarter (16 candidates)
+    static_assert(16 * NZ * ZS <= SCR, "staging fits the scratch");
+    double* st = scratch[wave];
+#pragma unroll
+    for (int qu = 0; qu < 4; ++qu) {
+      if ((lane >> 4) == qu) {
+        const int cl = lane & 15;
+#pragma unroll
+        for (int c = 0; c < NZ; ++c)
+#pragma unroll
+          for (int m = 0; m < ZS; ++m) st[(cl * NZ + c) * ZS + m] = (m < NP) ? Zc[c][m] : 0.0;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int r = qu * QT; r < (qu + 1) * QT; ++r) {
+        const int pr = 16 * r + (lane & 15) - qu * 16 * NZ;  // pair index within this quarter
+#pragma unroll
+        for (int kk = 0; kk < NK; ++kk) Af[r][kk] = st[pr * ZS + 4 * kk + (lane >> 4)];
+      }
+      __syncthreads();
+    }
+  }
+
   const double sigma2 = p.sigma2;
   const double rsig2 = 1.0 / sigma2;
 
@@ -161,7 +328,6 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
 #pragma unroll
       for (int j = 0; j < M; ++j) R[i][j] = sigma2 * 0.5 * (X[i][j] + X[j][i]);
   }
-  // Gi·(0, z̃) only needs the columns 1.. of G⁻¹ = R/σ²
 
   double beta[M], Pm[M][M];
   const bool init_ok = init_state<M, LEAD>(p, beta, Pm);
@@ -170,12 +336,19 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   double sumq = 0.0;
   bool neg = false;
   double last_det = 0.0, last_q = 0.0;  // fresh model: F = 0, F⁻¹ = 0, v = 0 (kalmanbasemodel.jl:65-67)
+  const int my_steps = nobs - 1;
+
+  // wave-uniform facts for the fast path
+  int wmin = live ? my_steps : 0x7fffffff;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) wmin = min(wmin, __shfl_xor(wmin, off));
+  const int wave_min_steps = __builtin_amdgcn_readfirstlane(wmin);
+  const bool wave_all_collapsed = __ballot(!collapsed) == 0ull;
 
   __syncthreads();
   const int nsteps = max(s_nobs_max - 1, 0);
-  const int my_steps = nobs - 1;
-  const int nchunks = (nsteps + kTC - 1) / kTC;
 
+  // ---- panel staging: LDS holds chunks c and c+1 while chunk c is processed ----------
   double pre[PER];
   auto load_chunk = [&](int c) {
     const size_t base = (size_t)c * CH;
@@ -187,225 +360,195 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
       pre[r] = (e < CH && g < lim) ? panel[g] : 0.0;
     }
   };
-  if (nchunks > 0) load_chunk(0);
-
-  for (int c = 0; c < nchunks; ++c) {
-    double* buf = sh[c & 1];
+  auto store_chunk = [&](double* buf) {
 #pragma unroll
     for (int r = 0; r < PER; ++r) {
       const int e = r * kBlock + tid;
       if (e < CH) buf[e] = pre[r];
     }
+  };
+  if (nsteps > 0) {
+    load_chunk(0);
+    store_chunk(sh[0]);
+    load_chunk(1);
+    store_chunk(sh[1]);
     __syncthreads();
-    if (c + 1 < nchunks) load_chunk(c + 1);
+    load_chunk(2);
+  }
+  auto col_of = [&](int t) -> const double* { return sh[(t / kTC) & 1] + (t % kTC) * LDP; };
 
-    const int tend = min(kTC, nsteps - c * kTC);
-    for (int tt = 0; tt < tend; ++tt) {
-      const int t = c * kTC + tt;  // 0-based step; reads column t (Julia t+1)
-      const double* col = buf + tt * LDP;
-      const double2 meta = *reinterpret_cast<const double2*>(col + NP + 2);  // (nanflag, y'y)
-      const bool act = t < my_steps;
-      if (!act) continue;
-      const bool acc = t >= 1;  // Julia t > 1 (filter.jl:194)
-
-      if (meta.x != 0.0) {
-        // NaN column: prediction only (filter.jl:126-140); F, v stale → the loglik
-        // re-adds the previous term (filter.jl:195 reads base.F / base.v unchanged).
-        double nb[M];
+  // one filter step given z̃_t (zc), (ȳ, ỹ'ỹ) and (nanflag, y'y) of column t
+  auto do_step = [&](int t, const double (&zc)[NZ], double2 yb_c, double2 meta_c) {
+    const bool fast = (t >= 1) && (meta_c.x == 0.0) && (t < wave_min_steps) && wave_all_collapsed;
+    if (fast) {
+      double bf[M], Pf[M][M], det, q;
+      collapsed_update<M>(zc, yb_c.x, yb_c.y, R, rsig2, beta, Pm, bf, Pf, det, q);
+      propagate<M, LEAD>(p, bf, Pf, beta, Pm);
+      last_det = det;
+      last_q = q;
+      ld.mul(det);
+      sumq += q;
+      neg = neg || (det < 0.0);
+      return;
+    }
+    const bool act = t < my_steps;
+    const bool acc = t >= 1;  // Julia t > 1 (filter.jl:194)
+    if (!act) return;
+    if (meta_c.x != 0.0) {
+      // NaN column: prediction only (filter.jl:126-140); F, v stale → the loglik
+      // re-adds the previous term (filter.jl:195 reads base.F / base.v unchanged).
+      double Pf[M][M];
 #pragma unroll
-        for (int i = 0; i < M; ++i) {
-          double s = p.delta[i];
+      for (int i = 0; i < M; ++i)
 #pragma unroll
-          for (int j = 0; j < M; ++j) s = fma(p.Phi[i][j], beta[j], s);
-          nb[i] = s;
-        }
-        double A[M][M];
+        for (int j = i; j < M; ++j) Pf[i][j] = Pm[i][j];
+      double bf[M];
 #pragma unroll
-        for (int i = 0; i < M; ++i)
-#pragma unroll
-          for (int j = 0; j < M; ++j) {
-            double s = 0.0;
-#pragma unroll
-            for (int l = 0; l < M; ++l) s = fma(p.Phi[i][l], Pm[l][j], s);
-            A[i][j] = s;
-          }
-#pragma unroll
-        for (int i = 0; i < M; ++i) {
-          beta[i] = nb[i];
-#pragma unroll
-          for (int j = i; j < M; ++j) {
-            double s = p.Q[i][j];
-#pragma unroll
-            for (int l = 0; l < M; ++l) s = fma(A[i][l], p.Phi[j][l], s);
-            Pm[i][j] = s;
-            Pm[j][i] = s;
-          }
-        }
-        if (acc) {
-          ld.mul(last_det);
-          sumq += last_q;
-          neg = neg || (last_det < 0.0);
-        }
-      } else {
-        // ---- z̃ = Z'ỹ_t for the non-constant columns (Σỹ = 0) ----
-        const double2 yb = *reinterpret_cast<const double2*>(col + NP);  // (ȳ, ỹ'ỹ)
-        double zt[NZ];
-        {
-          double a[NZ][2];
-#pragma unroll
-          for (int cz = 0; cz < NZ; ++cz) { a[cz][0] = 0.0; a[cz][1] = 0.0; }
-#pragma unroll
-          for (int i = 0; i < NP; i += 2) {
-            const double2 y2 = *reinterpret_cast<const double2*>(col + i);
-#pragma unroll
-            for (int cz = 0; cz < NZ; ++cz) {
-              a[cz][0] = fma(Zc[cz][i], y2.x, a[cz][0]);
-              a[cz][1] = fma(Zc[cz][i + 1], y2.y, a[cz][1]);
-            }
-          }
-#pragma unroll
-          for (int cz = 0; cz < NZ; ++cz) zt[cz] = a[cz][0] + a[cz][1];
-        }
-        double det, q;
-        double bf[M];   // β_{t|t}
-        double Pf[M][M];  // P_{t|t}
-        if (collapsed) {
-          // ĉ = G⁻¹ (0, z̃) + ȳ e₀ ;  r'r = ỹ'ỹ − z̃'ĉ[1:]
-          double ch[M];
-#pragma unroll
-          for (int i = 0; i < M; ++i) {
-            double s = 0.0;
-#pragma unroll
-            for (int j = 1; j < M; ++j) s = fma(R[i][j], zt[j - 1], s);
-            ch[i] = s * rsig2;
-          }
-          double rr = yb.y;
-#pragma unroll
-          for (int j = 1; j < M; ++j) rr = fma(-zt[j - 1], ch[j], rr);
-          ch[0] += yb.x;
-          double S[M][M];
-          double X[M][M + 1];  // [c | R] → [S⁻¹c | S⁻¹R]
-#pragma unroll
-          for (int i = 0; i < M; ++i) {
-#pragma unroll
-            for (int j = 0; j < M; ++j) {
-              S[i][j] = Pm[i][j] + R[i][j];
-              X[i][j + 1] = R[i][j];
-            }
-            X[i][0] = ch[i] - beta[i];
-          }
-          det = ldlt_solve<M, M + 1>(S, X);
-          double cx = 0.0;
-#pragma unroll
-          for (int i = 0; i < M; ++i) cx = fma(ch[i] - beta[i], X[i][0], cx);
-          q = fma(rr, rsig2, cx);
-#pragma unroll
-          for (int i = 0; i < M; ++i) {
-            double s = beta[i];
-#pragma unroll
-            for (int k = 0; k < M; ++k) s = fma(Pm[i][k], X[k][0], s);
-            bf[i] = s;
-          }
-#pragma unroll
-          for (int i = 0; i < M; ++i)
-#pragma unroll
-            for (int j = i; j < M; ++j) {
-              double s = 0.0;
-#pragma unroll
-              for (int k = 0; k < M; ++k) s = fma(Pm[i][k], X[k][j + 1], s);
-              Pf[i][j] = s;
-              Pf[j][i] = s;
-            }
-        } else {
-          // capacitance form on uncentered sums: Z'y = (Nȳ, z̃ + ȳ G[1:,0]), y'y
-          double zy[M];
-          zy[0] = (double)N * yb.x;
-#pragma unroll
-          for (int j = 1; j < M; ++j) zy[j] = fma(yb.x, G[j][0], zt[j - 1]);
-          double u[M];
-          double bgb = 0.0, bzy = 0.0;
-#pragma unroll
-          for (int i = 0; i < M; ++i) {
-            double g = 0.0;
-#pragma unroll
-            for (int j = 0; j < M; ++j) g = fma(G[i][j], beta[j], g);
-            u[i] = zy[i] - g;
-            bgb = fma(beta[i], g, bgb);
-            bzy = fma(beta[i], zy[i], bzy);
-          }
-          const double vv = fma(-2.0, bzy, meta.y) + bgb;
-          double W[M][M];
-          Capacitance<M>::solve(Pm, G, sigma2, W, det);
-#pragma unroll
-          for (int i = 0; i < M; ++i)
-#pragma unroll
-            for (int j = 0; j < i; ++j) W[i][j] = W[j][i];
-          double uk = 0.0;
-#pragma unroll
-          for (int i = 0; i < M; ++i) {
-            double s = 0.0;
-#pragma unroll
-            for (int j = 0; j < M; ++j) s = fma(W[i][j], u[j], s);
-            bf[i] = beta[i] + s;
-            uk = fma(u[i], s, uk);
-          }
-          q = (vv - uk) * rsig2;
-#pragma unroll
-          for (int i = 0; i < M; ++i)
-#pragma unroll
-            for (int j = 0; j < M; ++j) Pf[i][j] = sigma2 * W[i][j];
-        }
-
-        const bool upd = !(t == 0 && det == 0.0);  // inv(F) threw at t=1: skip update (filter.jl:151-154)
-        if (upd) {
-#pragma unroll
-          for (int i = 0; i < M; ++i) {  // β ← δ + Φ β_{t|t}   (filter.jl:162-165)
-            double s = p.delta[i];
-#pragma unroll
-            for (int j = 0; j < M; ++j) s = fma(p.Phi[i][j], bf[j], s);
-            beta[i] = s;
-          }
-          // P ← Φ P_{t|t} Φ' + Q   (≡ Φ(I − KZ)PΦ' + Q, filter.jl:168-176)
-          double A[M][M];
-#pragma unroll
-          for (int i = 0; i < M; ++i)
-#pragma unroll
-            for (int j = 0; j < M; ++j) {
-              double s = 0.0;
-#pragma unroll
-              for (int l = 0; l < M; ++l) s = fma(p.Phi[i][l], Pf[l][j], s);
-              A[i][j] = s;
-            }
-#pragma unroll
-          for (int i = 0; i < M; ++i)
-#pragma unroll
-            for (int j = i; j < M; ++j) {
-              double s = p.Q[i][j];
-#pragma unroll
-              for (int l = 0; l < M; ++l) s = fma(A[i][l], p.Phi[j][l], s);
-              Pm[i][j] = s;
-              Pm[j][i] = s;
-            }
-        }
-        last_det = det;
-        last_q = upd ? q : __builtin_nan("");
-        if (acc) {
-          ld.mul(det);
-          sumq += last_q;
-          neg = neg || (det < 0.0);
-        }
+      for (int i = 0; i < M; ++i) bf[i] = beta[i];
+      propagate<M, LEAD>(p, bf, Pf, beta, Pm);
+      if (acc) {
+        ld.mul(last_det);
+        sumq += last_q;
+        neg = neg || (last_det < 0.0);
       }
-      if constexpr (RECORD) {
-        if (live) {
-          const size_t o = (size_t)b * (size_t)(T - 1) + t;
+      return;
+    }
+    double det, q;
+    double bf[M];
+    double Pf[M][M];
+    if (collapsed) {
+      collapsed_update<M>(zc, yb_c.x, yb_c.y, R, rsig2, beta, Pm, bf, Pf, det, q);
+    } else {
+      // capacitance form on uncentered sums: Z'y = (Nȳ, z̃ + ȳ G[1:,0]), y'y
+      double zy[M];
+      zy[0] = (double)N * yb_c.x;
 #pragma unroll
-          for (int i = 0; i < M; ++i) rec_beta[o * M + i] = beta[i];
+      for (int j = 1; j < M; ++j) zy[j] = fma(yb_c.x, G[j][0], zc[j - 1]);
+      double u[M];
+      double bgb = 0.0, bzy = 0.0;
 #pragma unroll
-          for (int j = 0; j < M; ++j)
+      for (int i = 0; i < M; ++i) {
+        double g = 0.0;
 #pragma unroll
-            for (int i = 0; i < M; ++i) rec_P[o * M * M + j * M + i] = Pm[i][j];
-        }
+        for (int j = 0; j < M; ++j) g = fma(G[i][j], beta[j], g);
+        u[i] = zy[i] - g;
+        bgb = fma(beta[i], g, bgb);
+        bzy = fma(beta[i], zy[i], bzy);
       }
+      const double vv = fma(-2.0, bzy, meta_c.y) + bgb;
+      double W[M][M];
+      Capacitance<M>::solve(Pm, G, sigma2, W, det);
+#pragma unroll
+      for (int i = 0; i < M; ++i)
+#pragma unroll
+        for (int j = 0; j < i; ++j) W[i][j] = W[j][i];
+      double uk = 0.0;
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        double s = 0.0;
+#pragma unroll
+        for (int j = 0; j < M; ++j) s = fma(W[i][j], u[j], s);
+        bf[i] = beta[i] + s;
+        uk = fma(u[i], s, uk);
+      }
+      q = (vv - uk) * rsig2;
+#pragma unroll
+      for (int i = 0; i < M; ++i)
+#pragma unroll
+        for (int j = i; j < M; ++j) Pf[i][j] = sigma2 * W[i][j];
+    }
+    const bool upd = !(t == 0 && det == 0.0);  // inv(F) threw at t=1: skip update (filter.jl:151-154)
+    if (upd) propagate<M, LEAD>(p, bf, Pf, beta, Pm);
+    last_det = det;
+    last_q = upd ? q : __builtin_nan("");
+    if (acc) {
+      ld.mul(det);
+      sumq += last_q;
+      neg = neg || (det < 0.0);
+    }
+  };
+  auto record = [&](int t) {
+    if constexpr (RECORD) {
+      if (live && t < my_steps) {
+        const size_t o = (size_t)b * (size_t)(T - 1) + t;
+#pragma unroll
+        for (int i = 0; i < M; ++i) rec_beta[o * M + i] = beta[i];
+#pragma unroll
+        for (int j = 0; j < M; ++j)
+#pragma unroll
+          for (int i = 0; i < M; ++i) rec_P[o * M * M + j * M + i] = Pm[i][j];
+      }
+    }
+  };
+  auto rotate = [&](int t) {  // after step t: if chunk c = t / kTC is done, its buffer takes chunk c + 2
+    if ((t + 1) % kTC == 0) {
+      const int c = t / kTC;
+      __syncthreads();
+      store_chunk(sh[c & 1]);
+      __syncthreads();
+      load_chunk(c + 3);
+    }
+  };
+
+  if constexpr (USE_MFMA) {
+    double* scr = scratch[wave];
+    for (int t0 = 0; t0 < nsteps; t0 += TB) {
+      // ---- z̃ for steps t0 .. t0+15 of all 64 candidates: 8·NK MFMAs ----
+      const double* cb = col_of(t0);  // TB consecutive columns of one chunk
+      yfm_double4 acc[NRT];
+#pragma unroll
+      for (int r = 0; r < NRT; ++r) acc[r] = yfm_double4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) {
+        const int m = 4 * kk + (lane >> 4);
+        const double bv = (m < NP) ? cb[(lane & 15) * LDP + m] : 0.0;  // B[k = m][col = step]
+#pragma unroll
+        for (int r = 0; r < NRT; ++r) acc[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(Af[r][kk], bv, acc[r], 0, 0, 0);
+      }
+      // D[row = pair][col = step]: lane l holds step l & 15, pairs 16r + (l >> 4) + 4q
+#pragma unroll
+      for (int r = 0; r < NRT; ++r)
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) scr[(lane & 15) * SS + 16 * r + (lane >> 4) + 4 * q4] = acc[r][q4];
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's scratch writes landed
+      __builtin_amdgcn_wave_barrier();
+      const int tend = min(TB, nsteps - t0);
+      for (int tt = 0; tt < tend; ++tt) {
+        const int t = t0 + tt;
+        const double* col = cb + tt * LDP;
+        const double2 z2 = *reinterpret_cast<const double2*>(scr + tt * SS + 2 * lane);  // pair 2·lane, 2·lane+1
+        const double zc[NZ] = {z2.x, z2.y};
+        const double2 yb = *reinterpret_cast<const double2*>(col + NP);
+        const double2 meta = *reinterpret_cast<const double2*>(col + NP + 2);
+        do_step(t, zc, yb, meta);
+        record(t);
+        rotate(t);
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();  // scratch reads done before the next block's writes
+    }
+  } else {
+    double zc[NZ];
+    double2 yb_c = make_double2(0.0, 0.0), meta_c = make_double2(0.0, 0.0);
+    if (nsteps > 0) {
+      const double* c0 = col_of(0);
+      dot_zt<NP, NZ>(c0, Zc, zc);
+      yb_c = *reinterpret_cast<const double2*>(c0 + NP);
+      meta_c = *reinterpret_cast<const double2*>(c0 + NP + 2);
+    }
+    for (int t = 0; t < nsteps; ++t) {
+      const double* cn = col_of(t + 1);  // t + 1 ≤ nsteps ≤ T − 1: a resident panel column
+      double zn[NZ];
+      dot_zt<NP, NZ>(cn, Zc, zn);
+      const double2 yb_n = *reinterpret_cast<const double2*>(cn + NP);
+      const double2 meta_n = *reinterpret_cast<const double2*>(cn + NP + 2);
+      do_step(t, zc, yb_c, meta_c);
+      record(t);
+#pragma unroll
+      for (int j = 0; j < NZ; ++j) zc[j] = zn[j];
+      yb_c = yb_n;
+      meta_c = meta_n;
+      rotate(t);
     }
   }
 
@@ -456,6 +599,7 @@ int fixedz_np_for(int N) {
   if (N <= 8) return 8;
   if (N <= 16) return 16;
   if (N <= 24) return 24;
+  if (N <= 30) return 30;
   if (N <= 32) return 32;
   if (N <= 48) return 48;
   if (N <= 64) return 64;
@@ -468,6 +612,7 @@ hipError_t launch_fixedz(int kind, const LaunchArgs& a) {
       case 8: return launch_fixedz_np<8, 3, 1>(a);
       case 16: return launch_fixedz_np<16, 3, 1>(a);
       case 24: return launch_fixedz_np<24, 3, 1>(a);
+      case 30: return launch_fixedz_np<30, 3, 1>(a);
       case 32: return launch_fixedz_np<32, 3, 1>(a);
       case 48: return launch_fixedz_np<48, 3, 1>(a);
       case 64: return launch_fixedz_np<64, 3, 1>(a);
@@ -477,6 +622,7 @@ hipError_t launch_fixedz(int kind, const LaunchArgs& a) {
       case 8: return launch_fixedz_np<8, 5, 2>(a);
       case 16: return launch_fixedz_np<16, 5, 2>(a);
       case 24: return launch_fixedz_np<24, 5, 2>(a);
+      case 30: return launch_fixedz_np<30, 5, 2>(a);
       case 32: return launch_fixedz_np<32, 5, 2>(a);
       case 48: return launch_fixedz_np<48, 5, 2>(a);
       case 64: return launch_fixedz_np<64, 5, 2>(a);

@@ -1,0 +1,95 @@
+"""Multi-GPU sharding of batched loglik evaluations (one process per GPU).
+
+The reference distributes work only across independent Julia processes that
+claim forecast origins through mkdir locks (`src/forecasting.jl:54-79`); there
+is no in-filter exchange.  Here every (θ, window) evaluation is independent, so a
+batch is split into contiguous per-rank shards with no data-path collective; the
+only collectives are
+
+* ``all_gather`` of the per-candidate logliks (RCCL over xGMI with the ``nccl``
+  backend; gloo on CPU for tests), and
+* an argmax reduction of the best candidate — RCCL has no argmax, so each rank
+  contributes (best loglik, global index) and the pairs are all-gathered.
+
+For expanding windows (config 4) the split is *within* each window
+(`window_shards`): every rank gets an equal slice of every window's candidates,
+which balances the T_use-dependent cost that a split by window would not.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def shard_range(n: int, world: int, rank: int) -> tuple[int, int]:
+    """Contiguous, balanced [lo, hi) of n items for `rank` (sizes differ by at most 1)."""
+    base, extra = divmod(n, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def window_shards(counts, world: int, rank: int) -> np.ndarray:
+    """Global indices this rank evaluates when window w owns `counts[w]` consecutive candidates:
+    the rank's balanced slice of every window, concatenated in window order."""
+    idx = []
+    off = 0
+    for c in counts:
+        lo, hi = shard_range(int(c), world, rank)
+        idx.append(np.arange(off + lo, off + hi))
+        off += int(c)
+    return np.concatenate(idx) if idx else np.zeros(0, dtype=np.int64)
+
+
+@dataclass
+class GatherResult:
+    loglik: torch.Tensor  # all candidates, global order
+    best_index: int
+    best_value: float
+
+
+def gather_logliks(local: torch.Tensor, counts: list[int], group=None) -> torch.Tensor:
+    """All-gather per-rank loglik vectors of (possibly unequal) `counts` into global rank order."""
+    world = dist.get_world_size(group)
+    m = max(counts)
+    buf = torch.full((m,), float("nan"), dtype=local.dtype, device=local.device)
+    buf[: local.numel()] = local
+    out = torch.empty(world * m, dtype=local.dtype, device=local.device)
+    dist.all_gather_into_tensor(out, buf, group=group)
+    return torch.cat([out[r * m: r * m + counts[r]] for r in range(world)])
+
+
+def best_candidate(local: torch.Tensor, global_offset: int, group=None) -> tuple[int, float]:
+    """Global argmax of loglik over all ranks (NaN treated as -inf; ties → lowest global index)."""
+    v = torch.nan_to_num(local, nan=-float("inf"))
+    if v.numel():
+        i = int(torch.argmax(v).item())
+        pair = torch.tensor([float(v[i].item()), float(global_offset + i)], dtype=torch.float64, device=local.device)
+    else:
+        pair = torch.tensor([-float("inf"), float("inf")], dtype=torch.float64, device=local.device)
+    world = dist.get_world_size(group)
+    allp = torch.empty(2 * world, dtype=torch.float64, device=local.device)
+    dist.all_gather_into_tensor(allp, pair, group=group)
+    allp = allp.view(world, 2).cpu().numpy()
+    best = max(range(world), key=lambda r: (allp[r, 0], -allp[r, 1]))
+    return int(allp[best, 1]), float(allp[best, 0])
+
+
+def sharded_loglik(Theta: np.ndarray, evaluate: Callable[[np.ndarray], torch.Tensor], group=None,
+                   device=None) -> GatherResult:
+    """Evaluate Θ (P×B, identical on every rank) sharded over the group: rank r evaluates its
+    contiguous block with `evaluate` (a rank-local callable returning a tensor of logliks), then
+    the logliks are all-gathered and the best candidate reduced."""
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    B = Theta.shape[1]
+    lo, hi = shard_range(B, world, rank)
+    local = evaluate(np.asfortranarray(Theta[:, lo:hi]))
+    if device is not None:
+        local = local.to(device)
+    counts = [shard_range(B, world, r)[1] - shard_range(B, world, r)[0] for r in range(world)]
+    allv = gather_logliks(local, counts, group)
+    bi, bv = best_candidate(local, lo, group)
+    return GatherResult(allv, bi, bv)
