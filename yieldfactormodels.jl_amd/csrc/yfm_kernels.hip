@@ -201,7 +201,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   constexpr int CH = kTC * LDP;               // doubles per chunk
   constexpr int PER = (CH + kBlock - 1) / kBlock;
   constexpr int NZ = M - 1;                   // non-constant loading columns
-  constexpr bool USE_MFMA = (NZ == 2);
+  constexpr bool USE_MFMA = (NZ == 2) && (NP <= 32);  // fragments + LDS scratch budget
   constexpr int NK = (NP + 3) / 4;            // MFMA k-steps (4 maturities each)
   constexpr int NRT = 64 * NZ / 16;           // MFMA row tiles per wave (16 (cand, col) pairs each)
   constexpr int TB = 16;                      // steps per MFMA block
@@ -513,16 +513,23 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's scratch writes landed
       __builtin_amdgcn_wave_barrier();
       const int tend = min(TB, nsteps - t0);
+      // step operands for tt are read one step ahead (hides the LDS latency at 1 wave/SIMD)
+      double2 z2 = *reinterpret_cast<const double2*>(scr + 2 * lane);  // pairs 2·lane, 2·lane+1
+      double2 yb = *reinterpret_cast<const double2*>(cb + NP);
+      double2 meta = *reinterpret_cast<const double2*>(cb + NP + 2);
       for (int tt = 0; tt < tend; ++tt) {
         const int t = t0 + tt;
-        const double* col = cb + tt * LDP;
-        const double2 z2 = *reinterpret_cast<const double2*>(scr + tt * SS + 2 * lane);  // pair 2·lane, 2·lane+1
+        const int tn = min(tt + 1, TB - 1);
+        const double2 z2n = *reinterpret_cast<const double2*>(scr + tn * SS + 2 * lane);
+        const double2 ybn = *reinterpret_cast<const double2*>(cb + tn * LDP + NP);
+        const double2 metan = *reinterpret_cast<const double2*>(cb + tn * LDP + NP + 2);
         const double zc[NZ] = {z2.x, z2.y};
-        const double2 yb = *reinterpret_cast<const double2*>(col + NP);
-        const double2 meta = *reinterpret_cast<const double2*>(col + NP + 2);
         do_step(t, zc, yb, meta);
         record(t);
         rotate(t);
+        z2 = z2n;
+        yb = ybn;
+        meta = metan;
       }
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();  // scratch reads done before the next block's writes
