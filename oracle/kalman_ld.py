@@ -130,3 +130,92 @@ def loglik_ld(kind: int, maturities, Y, Theta, space: int = 0) -> np.ndarray:
     ll[neg | ~np.isfinite(ll)] = -np.inf
     ll[throws] = np.nan
     return ll
+
+
+def loglik_ld_tvl(maturities, Y, Theta, space: int = 0, T_use=None, dtype=LD) -> np.ndarray:
+    """TVλ EKF (filter.jl:12-80, tvλdns.jl:53-64) in extended precision, capacitance form,
+    batched over the columns of Θ (P×B); NaN where the reference throws.  NaN columns are
+    prediction-only steps whose loglik term repeats the previous one (stale F, v:
+    filter.jl:13-29, :195); T_use[b] restricts candidate b to data[:, 1:T_use[b]].
+    The Jacobian column keeps the reference's dZ1 = z/λ − z/(λ²m) (filter.jl:43)."""
+    from .kalman_oracle import KIND_TVL, transform_codes
+    M = 4
+    codes = np.asarray(transform_codes(KIND_TVL, M))
+    Theta = np.asarray(Theta, dtype=np.float64)
+    B = Theta.shape[1]
+    tc = _transform(codes[:, None].repeat(B, 1), Theta).astype(dtype) if space == 0 else Theta.astype(dtype)
+    sig2 = tc[0]
+    k = 1
+    U = np.zeros((B, M, M), dtype)
+    for j in range(M):
+        for i in range(j + 1):
+            U[:, i, j] = tc[k]
+            k += 1
+    Q = np.einsum("bli,blj->bij", U, U)
+    d = tc[k:k + M].T.copy()
+    k += M
+    Phi = tc[k:k + M * M].T.reshape(B, M, M).copy()
+    mats = np.asarray(maturities, dtype=np.float64).astype(dtype)
+    N = len(mats)
+    I = np.eye(M, dtype=dtype)
+    beta, det0 = _gesv(I - Phi, d[..., None])
+    beta = beta[..., 0]
+    K2 = np.eye(M * M, dtype=dtype)[None] - np.einsum("bij,bkl->bikjl", Phi, Phi).reshape(B, M * M, M * M)
+    vq = np.transpose(Q, (0, 2, 1)).reshape(B, M * M)
+    vp, det1 = _gesv(K2, vq[..., None])
+    P = np.transpose(vp[..., 0].reshape(B, M, M), (0, 2, 1))
+    throws = (det0 == 0) | (det1 == 0)
+    Y = np.asarray(Y, dtype=np.float64).astype(dtype)
+    T = Y.shape[1]
+    lsum = np.zeros(B, dtype)
+    qsum = np.zeros(B, dtype)
+    neg = np.zeros(B, bool)
+    Z = np.ones((B, N, M), dtype)
+    nobs = np.full(B, T) if T_use is None else np.asarray(T_use)
+    last_det = np.zeros(B, dtype)
+    last_q = np.zeros(B, dtype)
+    with np.errstate(all="ignore"):
+        for t in range(int(nobs.max()) - 1):
+            act = t < nobs - 1
+            if np.isnan(Y[:, t]).any():
+                beta_n = d + np.einsum("bij,bj->bi", Phi, beta)
+                P_n = Phi @ P @ np.transpose(Phi, (0, 2, 1)) + Q
+                beta = np.where(act[:, None], beta_n, beta)
+                P = np.where(act[:, None, None], P_n, P)
+                if t >= 1:
+                    lsum += np.where(act, np.log(np.abs(last_det)), 0)
+                    qsum += np.where(act, last_q, 0)
+                    neg |= act & (last_det < 0)
+                continue
+            lam = dtype(0.01) + np.exp(beta[:, 3])
+            tau = lam[:, None] * mats[None, :]
+            z = np.exp(-tau)
+            Z[:, :, 1] = (1 - z) / tau
+            Z[:, :, 2] = Z[:, :, 1] - z
+            dl = lam - dtype(0.01)
+            dz1 = z / lam[:, None] - z / (lam[:, None] ** 2 * mats[None, :])
+            dz2 = mats[None, :] * z
+            Z[:, :, 3] = ((beta[:, 1] + beta[:, 2])[:, None] * dz1 + beta[:, 2][:, None] * dz2) * dl[:, None]
+            r = Y[:, t][None, :] - np.einsum("bni,bi->bn", Z[:, :, :3], beta[:, :3])
+            u = np.einsum("bni,bn->bi", Z, r)
+            vv = np.einsum("bn,bn->b", r, r)
+            G = np.einsum("bni,bnj->bij", Z, Z)
+            Bt = sig2[:, None, None] * I + P @ G
+            W, det = _gesv(Bt, P)
+            W = (W + np.transpose(W, (0, 2, 1))) / 2
+            kv = np.einsum("bij,bj->bi", W, u)
+            q = (vv - np.einsum("bi,bi->b", u, kv)) / sig2
+            beta = np.where(act[:, None], d + np.einsum("bij,bj->bi", Phi, beta + kv), beta)
+            P = np.where(act[:, None, None], sig2[:, None, None] * (Phi @ W @ np.transpose(Phi, (0, 2, 1))) + Q, P)
+            last_det = np.where(act, det, last_det)
+            last_q = np.where(act, q, last_q)
+            if t >= 1:
+                lsum += np.where(act, np.log(np.abs(det)), 0)
+                qsum += np.where(act, q, 0)
+                neg |= act & (det < 0)
+        const = (N - M) * np.log(sig2) + N * np.log(2 * dtype(np.pi))
+        nterms = np.maximum(nobs - 2, 0)
+        ll = np.where(nterms > 0, -(nterms * const + lsum + qsum) / 2, 0).astype(np.float64)
+    ll[neg | ~np.isfinite(ll)] = -np.inf
+    ll[throws] = np.nan
+    return ll

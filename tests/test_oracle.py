@@ -136,10 +136,14 @@ def test_long_double_proxy_pinned_to_mp_truth(name):
     from oracle.kalman_ld import loglik_ld
     g = load_golden(name)
     kind = int(g["kind"])
-    if kind == KIND_TVL or np.isnan(g["Y"]).any():
-        pytest.skip("kalman_ld covers fixed-loading kinds on NaN-free panels")
+    if np.isnan(g["Y"]).any():
+        pytest.skip("kalman_ld covers NaN-free panels")
     k = len(g["ll_truth"])
-    got = loglik_ld(kind, g["maturities"], g["Y"], g["Theta"][:, :k], space=int(g["space"]))
+    if kind == KIND_TVL:
+        from oracle.kalman_ld import loglik_ld_tvl
+        got = loglik_ld_tvl(g["maturities"], g["Y"], g["Theta"][:, :k], space=int(g["space"]))
+    else:
+        got = loglik_ld(kind, g["maturities"], g["Y"], g["Theta"][:, :k], space=int(g["space"]))
     assert rel_err(got, g["ll_truth"]) <= 1e-11
 
 

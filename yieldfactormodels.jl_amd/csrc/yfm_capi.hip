@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -73,6 +74,7 @@ struct yfm_ctx {
   // staging for host-pointer calls
   DevBuf theta, out, tuse, rec_beta, rec_P;
   DevBuf flags;  // 2 × unsigned int
+  DevBuf scratch;  // per-candidate work records (TVλ init)
 };
 
 namespace {
@@ -92,7 +94,11 @@ int check_batch(yfm_ctx* ctx, int kind, int space, int P, int B) {
     return set_error(YFM_EINVAL, "P = %d but model_kind %d has %d parameters", P, kind, param_count(kind));
   if (B < 0) return set_error(YFM_EINVAL, "B = %d < 0", B);
   if (ctx->T <= 0) return set_error(YFM_ENOPANEL, "no panel: call yfm_set_panel first");
-  if (kind == YFM_MODEL_TVL) return set_error(YFM_EUNSUPPORTED, "TVλ kernel not built into this library yet");
+  if (kind == YFM_MODEL_TVL) {
+    if (ctx->N > yfm::tvl_max_n())
+      return set_error(YFM_EUNSUPPORTED, "N = %d maturities exceeds the TVλ kernel's %d", ctx->N, yfm::tvl_max_n());
+    return YFM_OK;
+  }
   if (yfm::fixedz_np_for(ctx->N) < 0)
     return set_error(YFM_EUNSUPPORTED, "N = %d maturities exceeds the fixed-loading kernel's 64", ctx->N);
   return YFM_OK;
@@ -108,17 +114,32 @@ int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int 
   a.B = B;
   a.space = space;
   a.panel = static_cast<const double*>(ctx->panel.p);
+  a.raw = static_cast<const double*>(ctx->raw.p);
   a.T = ctx->T;
   a.N = ctx->N;
   a.np = ctx->np;
+  a.ldp = ctx->ldp;
   a.mats = static_cast<const double*>(ctx->mats.p);
   a.T_use = d_T_use;
   a.out = d_out;
   a.flags = static_cast<unsigned int*>(ctx->flags.p);
   a.rec_beta = d_rb;
   a.rec_P = d_rP;
+  a.scratch = nullptr;
   a.stream = s;
-  hipError_t e = yfm::launch_fixedz(kind, a);
+  hipError_t e;
+  if (kind == YFM_MODEL_TVL) {
+    int lanes = yfm::tvl_lanes_for(B, ctx->N);
+    if (const char* ov = std::getenv("YFM_TVL_LANES")) {  // tuning override: 1, 2, 4, …, 64
+      const int l = std::atoi(ov);
+      if (l >= 1 && l <= 64 && (l & (l - 1)) == 0) lanes = l;
+    }
+    YFM_HIP_CHECK(ctx->scratch.ensure(yfm::tvl_scratch_bytes(B)));
+    a.scratch = static_cast<double*>(ctx->scratch.p);
+    e = yfm::launch_tvl(a, lanes);
+  } else {
+    e = yfm::launch_fixedz(kind, a);
+  }
   if (e != hipSuccess) return set_error(YFM_EHIP, "kernel launch: %s", hipGetErrorString(e));
   return YFM_OK;
 }
@@ -172,7 +193,7 @@ void yfm_destroy(yfm_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   for (DevBuf* b : {&ctx->panel, &ctx->mats, &ctx->raw, &ctx->theta, &ctx->out, &ctx->tuse, &ctx->rec_beta,
-                    &ctx->rec_P, &ctx->flags})
+                    &ctx->rec_P, &ctx->flags, &ctx->scratch})
     b->release();
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;

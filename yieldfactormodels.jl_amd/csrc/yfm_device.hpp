@@ -339,6 +339,39 @@ __device__ __forceinline__ double ldlt_solve(const double (&S)[M][M], double (&X
   return det;
 }
 
+// β ← δ + Φ β_{t|t};  P ← Φ P_{t|t} Φ' + Q   (filter.jl:162-176).  Pf: upper triangle.
+template <int M, int LEAD>
+__device__ __forceinline__ void propagate_state(const Params<M, LEAD>& p, const double (&bf)[M], const double (&Pf)[M][M],
+                                          double (&beta)[M], double (&Pm)[M][M]) {
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    double s = p.delta[i];
+#pragma unroll
+    for (int j = 0; j < M; ++j) s = fma(p.Phi[i][j], bf[j], s);
+    beta[i] = s;
+  }
+  double A[M][M];
+#pragma unroll
+  for (int i = 0; i < M; ++i)
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      double s = 0.0;
+#pragma unroll
+      for (int l = 0; l < M; ++l) s = fma(p.Phi[i][l], (l <= j) ? Pf[l][j] : Pf[j][l], s);
+      A[i][j] = s;
+    }
+#pragma unroll
+  for (int i = 0; i < M; ++i)
+#pragma unroll
+    for (int j = i; j < M; ++j) {
+      double s = p.Q[i][j];
+#pragma unroll
+      for (int l = 0; l < M; ++l) s = fma(A[i][l], p.Phi[j][l], s);
+      Pm[i][j] = s;
+      Pm[j][i] = s;
+    }
+}
+
 // log|∏ d_t| accumulated as mantissa × 2^expo: one multiply and two frexp
 // instructions per step instead of a software FP64 log.
 struct LogDetAcc {

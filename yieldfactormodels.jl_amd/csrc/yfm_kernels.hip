@@ -143,39 +143,6 @@ __device__ __forceinline__ void collapsed_update(const double (&zt)[M - 1], doub
     }
 }
 
-// β ← δ + Φ β_{t|t};  P ← Φ P_{t|t} Φ' + Q   (filter.jl:162-176).  Pf: upper triangle.
-template <int M, int LEAD>
-__device__ __forceinline__ void propagate(const Params<M, LEAD>& p, const double (&bf)[M], const double (&Pf)[M][M],
-                                          double (&beta)[M], double (&Pm)[M][M]) {
-#pragma unroll
-  for (int i = 0; i < M; ++i) {
-    double s = p.delta[i];
-#pragma unroll
-    for (int j = 0; j < M; ++j) s = fma(p.Phi[i][j], bf[j], s);
-    beta[i] = s;
-  }
-  double A[M][M];
-#pragma unroll
-  for (int i = 0; i < M; ++i)
-#pragma unroll
-    for (int j = 0; j < M; ++j) {
-      double s = 0.0;
-#pragma unroll
-      for (int l = 0; l < M; ++l) s = fma(p.Phi[i][l], (l <= j) ? Pf[l][j] : Pf[j][l], s);
-      A[i][j] = s;
-    }
-#pragma unroll
-  for (int i = 0; i < M; ++i)
-#pragma unroll
-    for (int j = i; j < M; ++j) {
-      double s = p.Q[i][j];
-#pragma unroll
-      for (int l = 0; l < M; ++l) s = fma(A[i][l], p.Phi[j][l], s);
-      Pm[i][j] = s;
-      Pm[j][i] = s;
-    }
-}
-
 typedef double yfm_double4 __attribute__((ext_vector_type(4)));
 
 // Fixed-loading models: DNS (M = 3, one γ, dns.jl:51-65) and the 5-factor
@@ -383,7 +350,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     if (fast) {
       double bf[M], Pf[M][M], det, q;
       collapsed_update<M>(zc, yb_c.x, yb_c.y, R, rsig2, beta, Pm, bf, Pf, det, q);
-      propagate<M, LEAD>(p, bf, Pf, beta, Pm);
+      propagate_state<M, LEAD>(p, bf, Pf, beta, Pm);
       last_det = det;
       last_q = q;
       ld.mul(det);
@@ -405,7 +372,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
       double bf[M];
 #pragma unroll
       for (int i = 0; i < M; ++i) bf[i] = beta[i];
-      propagate<M, LEAD>(p, bf, Pf, beta, Pm);
+      propagate_state<M, LEAD>(p, bf, Pf, beta, Pm);
       if (acc) {
         ld.mul(last_det);
         sumq += last_q;
@@ -458,7 +425,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
         for (int j = i; j < M; ++j) Pf[i][j] = sigma2 * W[i][j];
     }
     const bool upd = !(t == 0 && det == 0.0);  // inv(F) threw at t=1: skip update (filter.jl:151-154)
-    if (upd) propagate<M, LEAD>(p, bf, Pf, beta, Pm);
+    if (upd) propagate_state<M, LEAD>(p, bf, Pf, beta, Pm);
     last_det = det;
     last_q = upd ? q : __builtin_nan("");
     if (acc) {

@@ -1,0 +1,412 @@
+// yfm_tvl.hip — batched extended-Kalman-filter log-likelihood of the time-varying-λ
+// DNS model (TVλDNSModel) for gfx950.
+//
+// Restates, per candidate θ_b:
+//   get_loss                 src/models/kalman/filter.jl:182-209
+//   filter! (TVλ EKF)        src/models/kalman/filter.jl:12-80
+//   update_factor_loadings!  src/models/kalman/tvλdns.jl:53-64
+//   initialize_filter        src/models/kalman/filter.jl:1-10
+// with the reference's Jacobian column reproduced as written (filter.jl:43:
+// dZ1 = z/λ − z/(λ²m), not the true derivative).
+//
+// Mapping: ONE FILTER PER GROUP OF L LANES.  The state is
+// 4-dimensional but the loadings change every step (λ_t = 0.01 + exp(β₄)), so the
+// per-step work is O(N) in the maturities: lane j of a group owns maturities
+// i ≡ j (mod L), computes its share of the loadings Z (N×4), the innovation v and
+// the 14 sufficient statistics of the capacitance form —
+//     G = Z'Z (9 non-trivial entries; G₁₁ = N),  u = Z'v (4),  v'v (1)
+// — and the group reduces them with DPP / permlane butterflies (no LDS).  Every lane
+// of the group then runs the same 4×4 capacitance update redundantly, so the state
+// stays replicated in VGPRs and no broadcast is needed.  L is chosen per launch so
+// that B·L lanes fill the chip (B = 16,384 → L = 4; B = 1,024 → L = 64; B = 1 → L = 64).
+//
+// Capacitance form (nothing N×N is formed): B̃ = σ²I + P G, W = B̃⁻¹P,
+//   K v = W u,  P_{t|t} = σ² W,  v'F⁻¹v = (v'v − u'Wu)/σ²,
+//   log det F = (N−4) log σ² + log |det B̃|,  sign det F = sign det B̃.
+//
+// Panel: the caller's raw N×T column-major matrix (columns staged into LDS TC at a
+// time, prefetched into registers one chunk ahead) plus the per-column NaN flags of
+// the prepared panel (yfm_kernels.hip: prep_panel_kernel, offset np+2, stride ldp).
+#include "yfm_device.hpp"
+#include "yfm_internal.hpp"
+
+namespace yfm {
+
+namespace {
+
+constexpr int kTvlBlock = 256;
+constexpr int kTvlPre = 16;  // panel doubles prefetched per thread per chunk
+
+// x + (x of the partner lane) for the butterfly level `lvl` (partner distance 2^lvl,
+// every partner inside the same aligned group of 2^(lvl+1) lanes).
+template <int LVL>
+__device__ __forceinline__ double group_level_sum(double x) {
+  const int lo = __double2loint(x), hi = __double2hiint(x);
+  if constexpr (LVL == 0 || LVL == 1 || LVL == 2 || LVL == 3) {
+    // quad_perm xor1 / xor2, row_half_mirror, row_mirror
+    constexpr int ctrl = LVL == 0 ? 0xB1 : LVL == 1 ? 0x4E : LVL == 2 ? 0x141 : 0x140;
+    const int plo = __builtin_amdgcn_update_dpp(0, lo, ctrl, 0xf, 0xf, false);
+    const int phi = __builtin_amdgcn_update_dpp(0, hi, ctrl, 0xf, 0xf, false);
+    return x + __hiloint2double(phi, plo);
+  } else if constexpr (LVL == 4) {
+    // rows (0,1), (2,3): vdst' = [r0 r0 r2 r2], src' = [r1 r1 r3 r3]
+    const auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    return __hiloint2double(rh[0], rl[0]) + __hiloint2double(rh[1], rl[1]);
+  } else {
+    // halves: vdst' = [lo lo], src' = [hi hi]
+    const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    return __hiloint2double(rh[0], rl[0]) + __hiloint2double(rh[1], rl[1]);
+  }
+}
+
+// Sum over the aligned group of L lanes; every lane of the group receives the total.
+template <int L>
+__device__ __forceinline__ double group_sum(double x) {
+  if constexpr (L >= 2) x = group_level_sum<0>(x);
+  if constexpr (L >= 4) x = group_level_sum<1>(x);
+  if constexpr (L >= 8) x = group_level_sum<2>(x);
+  if constexpr (L >= 16) x = group_level_sum<3>(x);
+  if constexpr (L >= 32) x = group_level_sum<4>(x);
+  if constexpr (L >= 64) x = group_level_sum<5>(x);
+  return x;
+}
+
+}  // namespace
+
+// Sufficient statistics of one EKF step, indices into the accumulator array.
+enum : int { S2 = 0, S3, S4, G22, G23, G24, G33, G34, G44, U1, U2, U3, U4, VV, NSTAT };
+
+// Per-candidate record written by tvl_init_kernel: the decoded parameters and the
+// initial state, so the filter kernel never holds the 10×10 Lyapunov system in VGPRs.
+constexpr int kRecSigma = 0, kRecDelta = 1, kRecPhi = 5, kRecQ = 21, kRecBeta = 31, kRecP = 35, kRecOk = 45;
+constexpr int kRecLen = 48;  // doubles (padded to 16-byte multiples)
+
+// decode θ_b (transform_params + set_params!) and run initialize_filter (filter.jl:1-10)
+__global__ __launch_bounds__(256) void tvl_init_kernel(const double* __restrict__ theta, int P, int B, int space,
+                                                       double* __restrict__ rec) {
+  constexpr int M = 4;
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  Params<M, 0> p;
+  decode_params<M, 0>(theta + (size_t)b * P, space, p);
+  double beta[M], Pm[M][M];
+  const bool ok = init_state<M, 0>(p, beta, Pm);
+  double* r = rec + (size_t)b * kRecLen;
+  r[kRecSigma] = p.sigma2;
+  int q = 0;
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    r[kRecDelta + i] = p.delta[i];
+    r[kRecBeta + i] = beta[i];
+#pragma unroll
+    for (int k = 0; k < M; ++k) r[kRecPhi + i * M + k] = p.Phi[i][k];
+#pragma unroll
+    for (int k = i; k < M; ++k, ++q) {
+      r[kRecQ + q] = p.Q[i][k];
+      r[kRecP + q] = Pm[i][k];
+    }
+  }
+  r[kRecOk] = ok ? 1.0 : 0.0;
+  r[46] = 0.0;
+  r[47] = 0.0;
+}
+
+template <int L, bool RECORD>
+__global__ __launch_bounds__(kTvlBlock) void tvl_loglik_kernel(
+    const double* __restrict__ rec, int B, const double* __restrict__ Y,
+    const double* __restrict__ prep, int ldp, int np, int T, int N, int TC, const double* __restrict__ mats,
+    const int* __restrict__ T_use, double* __restrict__ out, unsigned int* __restrict__ flags,
+    double* __restrict__ rec_beta, double* __restrict__ rec_P) {
+  constexpr int M = 4;
+  constexpr int GPB = kTvlBlock / L;  // filters per block
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double* s_m = smem;            // maturities m_i
+  double* s_rm = smem + N;       // 1 / m_i
+  double* s_nan = smem + 2 * N;  // TC NaN flags of the staged chunk
+  double* s_y = s_nan + TC;      // TC columns of N yields (column-major, stride N)
+  __shared__ int s_nobs_max;
+
+  const int tid = threadIdx.x;
+  const int j = tid % L;
+  const int grp = tid / L;
+  const int b = blockIdx.x * GPB + grp;
+  const bool live = b < B;
+  const int bb = live ? b : (B - 1);
+  const int nobs = T_use ? T_use[bb] : T;
+
+  if (tid == 0) s_nobs_max = 0;
+  for (int i = tid; i < N; i += kTvlBlock) {
+    const double m = mats[i];
+    s_m[i] = m;
+    s_rm[i] = 1.0 / m;
+  }
+  __syncthreads();
+  atomicMax(&s_nobs_max, live ? nobs : 0);
+
+  Params<M, 0> p;
+  double beta[M], Pm[M][M];
+  bool init_ok;
+  {
+    const double* r = rec + (size_t)bb * kRecLen;
+    p.sigma2 = r[kRecSigma];
+    int q = 0;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      p.delta[i] = r[kRecDelta + i];
+      beta[i] = r[kRecBeta + i];
+#pragma unroll
+      for (int k = 0; k < M; ++k) p.Phi[i][k] = r[kRecPhi + i * M + k];
+#pragma unroll
+      for (int k = i; k < M; ++k, ++q) {
+        p.Q[i][k] = p.Q[k][i] = r[kRecQ + q];
+        Pm[i][k] = Pm[k][i] = r[kRecP + q];
+      }
+    }
+    init_ok = r[kRecOk] != 0.0;
+  }
+  const double sigma2 = p.sigma2;
+  const double rsig2 = 1.0 / sigma2;
+
+  LogDetAcc ld;
+  double sumq = 0.0;
+  bool neg = false;
+  double last_det = 0.0, last_q = 0.0;  // fresh model: F = 0, F⁻¹ = 0, v = 0 (kalmanbasemodel.jl:65-67)
+  const int my_steps = nobs - 1;
+
+  __syncthreads();
+  const int nsteps = max(s_nobs_max - 1, 0);
+  const int CHY = TC * N;  // yields per chunk
+
+  // ---- panel staging: chunk c (columns cTC .. cTC+TC-1) in LDS, chunk c+1 in registers ----
+  double pre[kTvlPre];
+  double pre_nan = 0.0;
+  auto load_chunk = [&](int c) {
+    const size_t base = (size_t)c * CHY;
+    const size_t lim = (size_t)T * N;
+#pragma unroll
+    for (int r = 0; r < kTvlPre; ++r) {
+      const int e = r * kTvlBlock + tid;
+      const size_t g = base + e;
+      pre[r] = (e < CHY && g < lim) ? Y[g] : 0.0;
+    }
+    const int tc = c * TC + tid;
+    pre_nan = (tid < TC && tc < T) ? prep[(size_t)tc * ldp + np + 2] : 0.0;
+  };
+  auto store_chunk = [&]() {
+#pragma unroll
+    for (int r = 0; r < kTvlPre; ++r) {
+      const int e = r * kTvlBlock + tid;
+      if (e < CHY) s_y[e] = pre[r];
+    }
+    if (tid < TC) s_nan[tid] = pre_nan;
+  };
+  if (nsteps > 0) {
+    load_chunk(0);
+    store_chunk();
+    __syncthreads();
+    load_chunk(1);
+  }
+
+  for (int t = 0; t < nsteps; ++t) {
+    const int tt = t % TC;
+    const bool act = t < my_steps;
+    const bool acc = t >= 1;  // Julia t > 1 (filter.jl:194)
+    const bool nan_col = s_nan[tt] != 0.0;
+    if (act && nan_col) {
+      // filter.jl:13-29: prediction only; F, F⁻¹, v stale → the loglik re-adds the last term
+      double bf[M], Pf[M][M];
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        bf[i] = beta[i];
+#pragma unroll
+        for (int k = i; k < M; ++k) Pf[i][k] = Pm[i][k];
+      }
+      propagate_state<M, 0>(p, bf, Pf, beta, Pm);
+      if (acc) {
+        ld.mul(last_det);
+        sumq += last_q;
+        neg = neg || (last_det < 0.0);
+      }
+    } else if (act) {
+      // ---- loadings and sufficient statistics over this lane's maturities ----
+      const double lam = 1e-2 + exp(beta[3]);  // tvλdns.jl:56
+      const double rl = 1.0 / lam;
+      const double dl = lam - 1e-2;            // filter.jl:38
+      const double c1 = (beta[1] + beta[2]) * dl;
+      const double c2 = beta[2] * dl;
+      const double* col = s_y + tt * N;
+      double s[NSTAT];
+#pragma unroll
+      for (int k = 0; k < NSTAT; ++k) s[k] = 0.0;
+#pragma unroll 2
+      for (int i = j; i < N; i += L) {
+        const double m = s_m[i];
+        const double it = rl * s_rm[i];          // 1/τ
+        const double z = exp(-(lam * m));        // z_i = e^{-τ_i}
+        const double z2 = (1.0 - z) * it;        // (1 − z)/τ
+        const double z3 = z2 - z;
+        const double zr = z * rl;                // z/λ
+        const double d1 = fma(-zr, it, zr);      // z/λ − z/(λ²m)   (filter.jl:43, as written)
+        const double d2 = m * z;                 // filter.jl:44
+        const double z4 = fma(c1, d1, c2 * d2);  // filter.jl:46
+        const double yh = fma(beta[2], z3, fma(beta[1], z2, beta[0]));  // Z[:,1:3] β[1:3]
+        const double v = col[i] - yh;
+        s[S2] += z2;
+        s[S3] += z3;
+        s[S4] += z4;
+        s[G22] = fma(z2, z2, s[G22]);
+        s[G23] = fma(z2, z3, s[G23]);
+        s[G24] = fma(z2, z4, s[G24]);
+        s[G33] = fma(z3, z3, s[G33]);
+        s[G34] = fma(z3, z4, s[G34]);
+        s[G44] = fma(z4, z4, s[G44]);
+        s[U1] += v;
+        s[U2] = fma(z2, v, s[U2]);
+        s[U3] = fma(z3, v, s[U3]);
+        s[U4] = fma(z4, v, s[U4]);
+        s[VV] = fma(v, v, s[VV]);
+      }
+#pragma unroll
+      for (int k = 0; k < NSTAT; ++k) s[k] = group_sum<L>(s[k]);
+
+      double G[M][M];
+      G[0][0] = (double)N;
+      G[0][1] = G[1][0] = s[S2];
+      G[0][2] = G[2][0] = s[S3];
+      G[0][3] = G[3][0] = s[S4];
+      G[1][1] = s[G22];
+      G[1][2] = G[2][1] = s[G23];
+      G[1][3] = G[3][1] = s[G24];
+      G[2][2] = s[G33];
+      G[2][3] = G[3][2] = s[G34];
+      G[3][3] = s[G44];
+      const double u[M] = {s[U1], s[U2], s[U3], s[U4]};
+
+      double W[M][M], det;
+      Capacitance<M>::solve(Pm, G, sigma2, W, det);
+#pragma unroll
+      for (int i = 0; i < M; ++i)
+#pragma unroll
+        for (int k = 0; k < i; ++k) W[i][k] = W[k][i];
+      double bf[M], Pf[M][M], uk = 0.0;
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        double w = 0.0;
+#pragma unroll
+        for (int k = 0; k < M; ++k) w = fma(W[i][k], u[k], w);
+        bf[i] = beta[i] + w;
+        uk = fma(u[i], w, uk);
+      }
+      const double q = (s[VV] - uk) * rsig2;
+#pragma unroll
+      for (int i = 0; i < M; ++i)
+#pragma unroll
+        for (int k = i; k < M; ++k) Pf[i][k] = sigma2 * W[i][k];
+      const bool upd = det != 0.0;  // inv(F) threw: return without updating (filter.jl:51-56)
+      if (upd) propagate_state<M, 0>(p, bf, Pf, beta, Pm);
+      last_det = det;
+      last_q = upd ? q : __builtin_nan("");
+      if (acc) {
+        ld.mul(det);
+        sumq += last_q;
+        neg = neg || (det < 0.0);
+      }
+    }
+    if constexpr (RECORD) {
+      if (live && act && j == 0) {
+        const size_t o = (size_t)b * (size_t)(T - 1) + t;
+#pragma unroll
+        for (int i = 0; i < M; ++i) rec_beta[o * M + i] = beta[i];
+#pragma unroll
+        for (int k = 0; k < M; ++k)
+#pragma unroll
+          for (int i = 0; i < M; ++i) rec_P[o * M * M + k * M + i] = Pm[i][k];
+      }
+    }
+    if (tt == TC - 1) {  // chunk done: its buffer takes the prefetched chunk, prefetch the one after
+      __syncthreads();
+      store_chunk();
+      __syncthreads();
+      load_chunk(t / TC + 2);
+    }
+  }
+
+  if (!live || j != 0) return;
+  double ll;
+  if (!init_ok) {
+    ll = __builtin_nan("");  // the reference throws from initialize_filter
+    atomicAdd(&flags[0], 1u);
+  } else {
+    const int nterms = max(nobs - 2, 0);
+    if (nterms == 0) {
+      ll = 0.0;
+    } else {
+      const double per_term = (double)(N - M) * log(sigma2) + (double)N * kLog2Pi;
+      ll = -0.5 * ((double)nterms * per_term + ld.log_value() + sumq);
+    }
+    if (neg || !isfinite(ll)) {  // DomainError / non-finite → -Inf (filter.jl:197-204)
+      ll = -__builtin_inf();
+      atomicAdd(&flags[1], 1u);
+    }
+  }
+  out[b] = ll;
+}
+
+namespace {
+
+template <int L>
+hipError_t launch_tvl_l(const LaunchArgs& a, int TC) {
+  constexpr int GPB = kTvlBlock / L;
+  const int grid = (a.B + GPB - 1) / GPB;
+  const size_t shmem = sizeof(double) * (size_t)(2 * a.N + TC + TC * a.N);
+  hipLaunchKernelGGL(tvl_init_kernel, dim3((a.B + 255) / 256), dim3(256), 0, a.stream, a.theta, a.P, a.B, a.space,
+                     a.scratch);
+  if (a.rec_beta) {
+    hipLaunchKernelGGL((tvl_loglik_kernel<L, true>), dim3(grid), dim3(kTvlBlock), shmem, a.stream, a.scratch, a.B,
+                       a.raw, a.panel, a.ldp, a.np, a.T, a.N, TC, a.mats, a.T_use, a.out, a.flags, a.rec_beta,
+                       a.rec_P);
+  } else {
+    hipLaunchKernelGGL((tvl_loglik_kernel<L, false>), dim3(grid), dim3(kTvlBlock), shmem, a.stream, a.scratch, a.B,
+                       a.raw, a.panel, a.ldp, a.np, a.T, a.N, TC, a.mats, a.T_use, a.out, a.flags, nullptr,
+                       nullptr);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace
+
+size_t tvl_scratch_bytes(int B) { return sizeof(double) * (size_t)kRecLen * (size_t)(B > 0 ? B : 1); }
+
+int tvl_max_n() { return (kTvlPre * kTvlBlock) - 1; }
+
+int tvl_lanes_for(int B, int N) {
+  // enough lanes for one wave per SIMD (256 CUs × 4 SIMDs × 64 lanes — the kernel's VGPR
+  // budget allows one), capped at a wave and at the maturity count rounded up to a power of two
+  long long want = (1024LL * 64 + B - 1) / (B > 0 ? B : 1);
+  int L = 1;
+  while (L < want && L < 64) L <<= 1;
+  int capN = 1;
+  while (capN < N && capN < 64) capN <<= 1;
+  return L < capN ? L : capN;
+}
+
+hipError_t launch_tvl(const LaunchArgs& a, int lanes) {
+  // columns per chunk: the prefetch registers hold ≤ kTvlPre·256 yields
+  int TC = (kTvlPre * kTvlBlock) / a.N;
+  if (TC > 32) TC = 32;
+  if (TC < 1) return hipErrorInvalidValue;
+  switch (lanes) {
+    case 1: return launch_tvl_l<1>(a, TC);
+    case 2: return launch_tvl_l<2>(a, TC);
+    case 4: return launch_tvl_l<4>(a, TC);
+    case 8: return launch_tvl_l<8>(a, TC);
+    case 16: return launch_tvl_l<16>(a, TC);
+    case 32: return launch_tvl_l<32>(a, TC);
+    case 64: return launch_tvl_l<64>(a, TC);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace yfm
