@@ -263,9 +263,10 @@ def set_params_base(s: KalmanState, params):
 
 def dns_loadings(gamma, maturities, Z):
     """dns.jl:51-65: λ = 0.01 + e^γ; z = e^{-λτ}; Z = [1, (1-z)/(λτ), (1-z)/(λτ) - z]."""
-    lam = 1e-2 + math.exp(gamma)
-    tau = lam * maturities
-    z = np.exp(-tau)
+    with np.errstate(all="ignore"):  # IEEE semantics like Julia: exp overflow → Inf, no exception
+        lam = np.float64(1e-2) + np.exp(np.float64(gamma))
+        tau = lam * maturities
+        z = np.exp(-tau)
     Z[:, 0] = 1.0
     Z[:, 1] = (1.0 - z) / tau
     Z[:, 2] = Z[:, 1] - z
@@ -275,18 +276,20 @@ def gns_loadings(gammas, maturities, Z):
     """5-factor generalised NS extension (not in the reference): [1, S(λ1), C(λ1), S(λ2), C(λ2)]."""
     Z[:, 0] = 1.0
     for b, g in enumerate(gammas):
-        lam = 1e-2 + math.exp(g)
-        tau = lam * maturities
-        z = np.exp(-tau)
+        with np.errstate(all="ignore"):
+            lam = np.float64(1e-2) + np.exp(np.float64(g))
+            tau = lam * maturities
+            z = np.exp(-tau)
         Z[:, 1 + 2 * b] = (1.0 - z) / tau
         Z[:, 2 + 2 * b] = Z[:, 1 + 2 * b] - z
 
 
 def tvl_loadings(s: KalmanState, beta4):
     """tvλdns.jl:53-64 (columns 2 and 3 only; column 1 stays ones)."""
-    s.lam = 1e-2 + math.exp(beta4)
-    tau = s.lam * s.maturities
-    s.z_i = np.exp(-tau)
+    with np.errstate(all="ignore"):
+        s.lam = np.float64(1e-2) + np.exp(np.float64(beta4))
+        tau = s.lam * s.maturities
+        s.z_i = np.exp(-tau)
     s.extra["tau"] = tau
     s.Z[:, 1] = (1.0 - s.z_i) / tau
     s.Z[:, 2] = s.Z[:, 1] - s.z_i

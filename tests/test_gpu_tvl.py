@@ -104,12 +104,13 @@ def test_tvl_config3_cross_section_vs_c_oracle(engine, config3):
     Th[:, 0] = S.theta0(KIND_TVL)
     ref = c_oracle(Y, mats, Th)
     truth = loglik_ld_tvl(mats, Y, Th)
+    alt = loglik_ld_tvl(mats, Y, Th, dtype=np.float64)
     engine.set_panel(Y, mats)
     got = engine.loglik(KIND_TVL, Th)
-    assert_parity(got, ref, truth)
+    assert_parity(got, ref, truth, alt=alt)
     for L in (1, 64):
         with lanes_override(L):
-            assert_parity(engine.loglik(KIND_TVL, Th), ref, truth)
+            assert_parity(engine.loglik(KIND_TVL, Th), ref, truth, alt=alt)
 
 
 def test_tvl_windows_nan_and_edges(engine, config3):
@@ -124,10 +125,11 @@ def test_tvl_windows_nan_and_edges(engine, config3):
     tu = np.array([1, 2, 3, 10, 40, 89, 90, 90, 64, 65, 33, 77], dtype=np.int32)
     ref = c_oracle(Yn, m, Th, T_use=tu)
     truth = loglik_ld_tvl(m, Yn, Th, T_use=tu)
+    alt = loglik_ld_tvl(m, Yn, Th, T_use=tu, dtype=np.float64)
     engine.set_panel(Yn, m)
     for L in (1, 4, 64):
         with lanes_override(L):
-            assert_parity(engine.loglik(KIND_TVL, Th, T_use=tu), ref, truth)
+            assert_parity(engine.loglik(KIND_TVL, Th, T_use=tu), ref, truth, alt=alt)
 
 
 def test_tvl_full_batch_properties(engine, config3):
@@ -158,3 +160,29 @@ def test_tvl_full_batch_properties(engine, config3):
     bound = np.maximum(1e-9, 100 * np.abs(fp64[fin] - truth[fin]) / np.abs(truth[fin]))
     for got in (a[perm[:48]], w64):
         assert np.all(np.abs(got[fin] - truth[fin]) / np.abs(truth[fin]) <= bound)
+
+
+@pytest.mark.parametrize("grid", ["wu30", "irregular"])
+def test_tvl_maturity_grids_and_exp_paths(engine, grid):
+    """The exp recurrence over maturity jumps (≤ 8 distinct m_{i+L} − m_i) vs one exp per maturity
+    (YFM_TVL_EXP=1, also the automatic fallback for irregular grids), against the C oracle + truth."""
+    if grid == "wu30":
+        mats = S.maturities_30()
+    else:
+        mats = np.sort(np.random.default_rng(3).uniform(1.0, 360.0, 24)).round(3)
+    Y = S.simulate_panel(KIND_TVL, 80, maturities=mats)
+    Th = S.theta_batch(KIND_TVL, 16, seed=43, bad_frac=0.0, scale=0.02)
+    ref = c_oracle(Y, mats, Th)
+    truth = loglik_ld_tvl(mats, Y, Th)
+    alt = loglik_ld_tvl(mats, Y, Th, dtype=np.float64)
+    engine.set_panel(Y, mats)
+    for L in (1, 4, 16):
+        with lanes_override(L):
+            rec = engine.loglik(KIND_TVL, Th)
+            os.environ["YFM_TVL_EXP"] = "1"
+            try:
+                ex = engine.loglik(KIND_TVL, Th)
+            finally:
+                os.environ.pop("YFM_TVL_EXP", None)
+        assert_parity(rec, ref, truth, alt=alt)
+        assert_parity(ex, ref, truth, alt=alt)

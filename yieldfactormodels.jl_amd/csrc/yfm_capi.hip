@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/yfm.h"
 #include "yfm_internal.hpp"
@@ -75,6 +76,10 @@ struct yfm_ctx {
   DevBuf theta, out, tuse, rec_beta, rec_P;
   DevBuf flags;  // 2 × unsigned int
   DevBuf scratch;  // per-candidate work records (TVλ init)
+  // TVλ maturity-jump tables, one per lane count L = 2^l (built lazily, reset by set_panel)
+  std::vector<double> mats_host;
+  int gap_K[7] = {-1, -1, -1, -1, -1, -1, -1};
+  DevBuf gap_buf[7];
 };
 
 namespace {
@@ -101,6 +106,50 @@ int check_batch(yfm_ctx* ctx, int kind, int space, int P, int B) {
   }
   if (yfm::fixedz_np_for(ctx->N) < 0)
     return set_error(YFM_EUNSUPPORTED, "N = %d maturities exceeds the fixed-loading kernel's 64", ctx->N);
+  return YFM_OK;
+}
+
+// Jump table of the TVλ exp recurrence for lane count L: distinct m_{i+L} − m_i (exact
+// equality) and each maturity's index; K = 0 when there are more than yfm::kTvlGaps.
+int tvl_gaps(yfm_ctx* ctx, int L, yfm::TvlGaps& g) {
+  int l = 0;
+  while ((1 << l) < L) ++l;
+  if (ctx->gap_K[l] < 0) {
+    const int N = ctx->N;
+    std::vector<double> d;
+    std::vector<int> idx(N, 0);
+    bool ok = true;
+    for (int i = 0; i + L < N && ok; ++i) {
+      const double gap = ctx->mats_host[i + L] - ctx->mats_host[i];
+      int k = 0;
+      while (k < (int)d.size() && d[k] != gap) ++k;
+      if (k == (int)d.size()) {
+        if ((int)d.size() == yfm::kTvlGaps) ok = false;
+        else d.push_back(gap);
+      }
+      idx[i] = k;
+    }
+    int K = ok ? (int)d.size() : 0;
+    if (K == 0 && ok) K = 1, d.push_back(0.0);  // N ≤ L: every lane has at most one maturity
+    d.resize(yfm::kTvlGaps, 0.0);
+    if (K > 0) {
+      YFM_HIP_CHECK(ctx->gap_buf[l].ensure(sizeof(double) * yfm::kTvlGaps + sizeof(int) * N));
+      char* base = static_cast<char*>(ctx->gap_buf[l].p);
+      YFM_HIP_CHECK(hipMemcpy(base, d.data(), sizeof(double) * yfm::kTvlGaps, hipMemcpyHostToDevice));
+      YFM_HIP_CHECK(hipMemcpy(base + sizeof(double) * yfm::kTvlGaps, idx.data(), sizeof(int) * N,
+                              hipMemcpyHostToDevice));
+    }
+    ctx->gap_K[l] = K;
+  }
+  g.K = ctx->gap_K[l];
+  if (g.K > 0) {
+    char* base = static_cast<char*>(ctx->gap_buf[l].p);
+    g.d = reinterpret_cast<const double*>(base);
+    g.idx = reinterpret_cast<const int*>(base + sizeof(double) * yfm::kTvlGaps);
+  }
+  if (const char* ov = std::getenv("YFM_TVL_EXP")) {  // diagnostic: force one exp per maturity
+    if (std::atoi(ov) == 1) g.K = 0;
+  }
   return YFM_OK;
 }
 
@@ -136,7 +185,9 @@ int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int 
     }
     YFM_HIP_CHECK(ctx->scratch.ensure(yfm::tvl_scratch_bytes(B)));
     a.scratch = static_cast<double*>(ctx->scratch.p);
-    e = yfm::launch_tvl(a, lanes);
+    yfm::TvlGaps g;
+    if (int r = tvl_gaps(ctx, lanes, g)) return r;
+    e = yfm::launch_tvl(a, g, lanes);
   } else {
     e = yfm::launch_fixedz(kind, a);
   }
@@ -195,6 +246,7 @@ void yfm_destroy(yfm_ctx* ctx) {
   for (DevBuf* b : {&ctx->panel, &ctx->mats, &ctx->raw, &ctx->theta, &ctx->out, &ctx->tuse, &ctx->rec_beta,
                     &ctx->rec_P, &ctx->flags, &ctx->scratch})
     b->release();
+  for (DevBuf& b : ctx->gap_buf) b.release();
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -216,6 +268,8 @@ int yfm_set_panel(yfm_ctx* ctx, const double* Y, int N, int T, const double* mat
   YFM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
   ctx->N = N;
   ctx->T = T;
+  ctx->mats_host.assign(maturities, maturities + N);
+  for (int& k : ctx->gap_K) k = -1;
   ctx->np = npad;
   ctx->ldp = ldp;
   return YFM_OK;

@@ -27,7 +27,16 @@ hipError_t launch_fixedz(int kind, const LaunchArgs& a);
 int tvl_lanes_for(int B, int N);
 int tvl_max_n();
 size_t tvl_scratch_bytes(int B);
-hipError_t launch_tvl(const LaunchArgs& a, int lanes);
+// Maturity jump table for the TVλ exp recurrence (built on the host per lane count L):
+// the distinct values d_k of m_{i+L} − m_i and, per maturity i, the index k of its jump.
+// K = 0 disables the recurrence (one exp per maturity).
+constexpr int kTvlGaps = 8;
+struct TvlGaps {
+  int K = 0;
+  const double* d = nullptr;  // device, kTvlGaps
+  const int* idx = nullptr;   // device, N
+};
+hipError_t launch_tvl(const LaunchArgs& a, const TvlGaps& g, int lanes);
 hipError_t launch_prep_panel(const double* Y, int N, int T, int np, int ldp, double* out, hipStream_t s);
 
 }  // namespace yfm

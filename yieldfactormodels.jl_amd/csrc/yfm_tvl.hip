@@ -117,15 +117,18 @@ template <int L, bool RECORD>
 __global__ __launch_bounds__(kTvlBlock) void tvl_loglik_kernel(
     const double* __restrict__ rec, int B, const double* __restrict__ Y,
     const double* __restrict__ prep, int ldp, int np, int T, int N, int TC, const double* __restrict__ mats,
+    int K, const double* __restrict__ gap_d, const int* __restrict__ gap_idx,
     const int* __restrict__ T_use, double* __restrict__ out, unsigned int* __restrict__ flags,
     double* __restrict__ rec_beta, double* __restrict__ rec_P) {
   constexpr int M = 4;
   constexpr int GPB = kTvlBlock / L;  // filters per block
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  double* s_m = smem;            // maturities m_i
-  double* s_rm = smem + N;       // 1 / m_i
-  double* s_nan = smem + 2 * N;  // TC NaN flags of the staged chunk
-  double* s_y = s_nan + TC;      // TC columns of N yields (column-major, stride N)
+  double2* s_mr = reinterpret_cast<double2*>(smem);  // (m_i, 1/m_i)
+  double* s_nan = smem + 2 * N;                       // TC NaN flags of the staged chunk
+  double* s_y = s_nan + TC;                           // TC columns of N yields (column-major, stride N)
+  double* s_w = s_y + TC * N;                         // per group: e^{-λ d_k}, k < K (≤ kTvlGaps)
+  int* s_gi = reinterpret_cast<int*>(s_w + GPB * kTvlGaps);  // gap index of the jump i → i + L
+  __shared__ double s_gd[kTvlGaps];
   __shared__ int s_nobs_max;
 
   const int tid = threadIdx.x;
@@ -139,9 +142,10 @@ __global__ __launch_bounds__(kTvlBlock) void tvl_loglik_kernel(
   if (tid == 0) s_nobs_max = 0;
   for (int i = tid; i < N; i += kTvlBlock) {
     const double m = mats[i];
-    s_m[i] = m;
-    s_rm[i] = 1.0 / m;
+    s_mr[i] = make_double2(m, 1.0 / m);
+    if (K > 0) s_gi[i] = gap_idx[i];
   }
+  if (tid < K) s_gd[tid] = gap_d[tid];
   __syncthreads();
   atomicMax(&s_nobs_max, live ? nobs : 0);
 
@@ -240,11 +244,10 @@ __global__ __launch_bounds__(kTvlBlock) void tvl_loglik_kernel(
       double s[NSTAT];
 #pragma unroll
       for (int k = 0; k < NSTAT; ++k) s[k] = 0.0;
-#pragma unroll 2
-      for (int i = j; i < N; i += L) {
-        const double m = s_m[i];
-        const double it = rl * s_rm[i];          // 1/τ
-        const double z = exp(-(lam * m));        // z_i = e^{-τ_i}
+      // one maturity: z = e^{-λm}, loadings, Jacobian column, innovation, statistics
+      auto accum = [&](double2 mr, double z, double y) {
+        const double m = mr.x;
+        const double it = rl * mr.y;             // 1/τ
         const double z2 = (1.0 - z) * it;        // (1 − z)/τ
         const double z3 = z2 - z;
         const double zr = z * rl;                // z/λ
@@ -252,7 +255,7 @@ __global__ __launch_bounds__(kTvlBlock) void tvl_loglik_kernel(
         const double d2 = m * z;                 // filter.jl:44
         const double z4 = fma(c1, d1, c2 * d2);  // filter.jl:46
         const double yh = fma(beta[2], z3, fma(beta[1], z2, beta[0]));  // Z[:,1:3] β[1:3]
-        const double v = col[i] - yh;
+        const double v = y - yh;
         s[S2] += z2;
         s[S3] += z3;
         s[S4] += z4;
@@ -267,6 +270,29 @@ __global__ __launch_bounds__(kTvlBlock) void tvl_loglik_kernel(
         s[U3] = fma(z3, v, s[U3]);
         s[U4] = fma(z4, v, s[U4]);
         s[VV] = fma(v, v, s[VV]);
+      };
+      if (K > 0) {
+        // few distinct jumps d_k = m_{i+L} − m_i: z_{i+L} = z_i · e^{-λ d_k}, one exp per lane
+        // plus K per group instead of one per maturity (relative drift ≤ (N/L) ulp)
+        double* w = s_w + grp * kTvlGaps;
+        for (int q = j; q < K; q += L) w[q] = exp(-(lam * s_gd[q]));
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double z = (j < N) ? exp(-(lam * s_mr[j].x)) : 0.0;
+#pragma unroll 2
+        for (int i = j; i < N; i += L) {
+          const double2 mr = s_mr[i];
+          const double wn = w[s_gi[i]];
+          accum(mr, z, col[i]);
+          z *= wn;
+        }
+      } else {
+#pragma unroll 2
+        for (int i = j; i < N; i += L) {
+          const double2 mr = s_mr[i];
+          accum(mr, exp(-(lam * mr.x)), col[i]);  // z_i = e^{-τ_i}
+        }
       }
 #pragma unroll
       for (int k = 0; k < NSTAT; ++k) s[k] = group_sum<L>(s[k]);
@@ -357,19 +383,19 @@ __global__ __launch_bounds__(kTvlBlock) void tvl_loglik_kernel(
 namespace {
 
 template <int L>
-hipError_t launch_tvl_l(const LaunchArgs& a, int TC) {
+hipError_t launch_tvl_l(const LaunchArgs& a, const TvlGaps& g, int TC) {
   constexpr int GPB = kTvlBlock / L;
   const int grid = (a.B + GPB - 1) / GPB;
-  const size_t shmem = sizeof(double) * (size_t)(2 * a.N + TC + TC * a.N);
+  const size_t shmem = sizeof(double) * (size_t)(2 * a.N + TC + TC * a.N + GPB * kTvlGaps) + sizeof(int) * a.N;
   hipLaunchKernelGGL(tvl_init_kernel, dim3((a.B + 255) / 256), dim3(256), 0, a.stream, a.theta, a.P, a.B, a.space,
                      a.scratch);
   if (a.rec_beta) {
     hipLaunchKernelGGL((tvl_loglik_kernel<L, true>), dim3(grid), dim3(kTvlBlock), shmem, a.stream, a.scratch, a.B,
-                       a.raw, a.panel, a.ldp, a.np, a.T, a.N, TC, a.mats, a.T_use, a.out, a.flags, a.rec_beta,
+                       a.raw, a.panel, a.ldp, a.np, a.T, a.N, TC, a.mats, g.K, g.d, g.idx, a.T_use, a.out, a.flags, a.rec_beta,
                        a.rec_P);
   } else {
     hipLaunchKernelGGL((tvl_loglik_kernel<L, false>), dim3(grid), dim3(kTvlBlock), shmem, a.stream, a.scratch, a.B,
-                       a.raw, a.panel, a.ldp, a.np, a.T, a.N, TC, a.mats, a.T_use, a.out, a.flags, nullptr,
+                       a.raw, a.panel, a.ldp, a.np, a.T, a.N, TC, a.mats, g.K, g.d, g.idx, a.T_use, a.out, a.flags, nullptr,
                        nullptr);
   }
   return hipGetLastError();
@@ -392,19 +418,19 @@ int tvl_lanes_for(int B, int N) {
   return L < capN ? L : capN;
 }
 
-hipError_t launch_tvl(const LaunchArgs& a, int lanes) {
+hipError_t launch_tvl(const LaunchArgs& a, const TvlGaps& g, int lanes) {
   // columns per chunk: the prefetch registers hold ≤ kTvlPre·256 yields
   int TC = (kTvlPre * kTvlBlock) / a.N;
   if (TC > 32) TC = 32;
   if (TC < 1) return hipErrorInvalidValue;
   switch (lanes) {
-    case 1: return launch_tvl_l<1>(a, TC);
-    case 2: return launch_tvl_l<2>(a, TC);
-    case 4: return launch_tvl_l<4>(a, TC);
-    case 8: return launch_tvl_l<8>(a, TC);
-    case 16: return launch_tvl_l<16>(a, TC);
-    case 32: return launch_tvl_l<32>(a, TC);
-    case 64: return launch_tvl_l<64>(a, TC);
+    case 1: return launch_tvl_l<1>(a, g, TC);
+    case 2: return launch_tvl_l<2>(a, g, TC);
+    case 4: return launch_tvl_l<4>(a, g, TC);
+    case 8: return launch_tvl_l<8>(a, g, TC);
+    case 16: return launch_tvl_l<16>(a, g, TC);
+    case 32: return launch_tvl_l<32>(a, g, TC);
+    case 64: return launch_tvl_l<64>(a, g, TC);
   }
   return hipErrorInvalidValue;
 }
