@@ -36,6 +36,15 @@ ID, POS, R11 = 0, 1, 2
 KIND_DNS, KIND_TVL, KIND_GNS = 0, 1, 2
 
 
+def exp_ieee(x):
+    """math.exp with Julia's IEEE overflow (Inf) instead of Python's OverflowError."""
+    x = float(x)
+    try:
+        return math.exp(x)
+    except OverflowError:
+        return math.inf
+
+
 class SingularException(Exception):
     """Julia's LinearAlgebra.SingularException (thrown by `\\` / `inv`)."""
 
@@ -263,8 +272,8 @@ def set_params_base(s: KalmanState, params):
 
 def dns_loadings(gamma, maturities, Z):
     """dns.jl:51-65: λ = 0.01 + e^γ; z = e^{-λτ}; Z = [1, (1-z)/(λτ), (1-z)/(λτ) - z]."""
-    with np.errstate(all="ignore"):  # IEEE semantics like Julia: exp overflow → Inf, no exception
-        lam = np.float64(1e-2) + np.exp(np.float64(gamma))
+    lam = 1e-2 + exp_ieee(gamma)
+    with np.errstate(all="ignore"):
         tau = lam * maturities
         z = np.exp(-tau)
     Z[:, 0] = 1.0
@@ -276,8 +285,8 @@ def gns_loadings(gammas, maturities, Z):
     """5-factor generalised NS extension (not in the reference): [1, S(λ1), C(λ1), S(λ2), C(λ2)]."""
     Z[:, 0] = 1.0
     for b, g in enumerate(gammas):
+        lam = 1e-2 + exp_ieee(g)
         with np.errstate(all="ignore"):
-            lam = np.float64(1e-2) + np.exp(np.float64(g))
             tau = lam * maturities
             z = np.exp(-tau)
         Z[:, 1 + 2 * b] = (1.0 - z) / tau
@@ -286,8 +295,8 @@ def gns_loadings(gammas, maturities, Z):
 
 def tvl_loadings(s: KalmanState, beta4):
     """tvλdns.jl:53-64 (columns 2 and 3 only; column 1 stays ones)."""
+    s.lam = 1e-2 + exp_ieee(beta4)
     with np.errstate(all="ignore"):
-        s.lam = np.float64(1e-2) + np.exp(np.float64(beta4))
         tau = s.lam * s.maturities
         s.z_i = np.exp(-tau)
     s.extra["tau"] = tau
@@ -368,7 +377,7 @@ def filter_step_tvl(s: KalmanState, y):
     s.v = y - s.y_pred  # :34
     dlam = s.lam - 1e-2  # :38
     m = s.maturities
-    dZ1 = s.z_i / s.lam - s.z_i / (s.lam ** 2 * m)  # :43 (quirk kept)
+    dZ1 = s.z_i / s.lam - s.z_i / ((s.lam * s.lam) * m)  # :43 (quirk kept; λ^2 = λ*λ, Inf on overflow)
     dZ2 = m * s.z_i  # :44
     s.Z[:, 3] = ((s.beta[1] + s.beta[2]) * dZ1 + s.beta[2] * dZ2) * dlam  # :46
     s.F = (s.Z @ s.P) @ s.Z.T + s.Omega_obs  # :49
