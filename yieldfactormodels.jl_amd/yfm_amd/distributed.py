@@ -78,6 +78,21 @@ def best_candidate(local: torch.Tensor, global_offset: int, group=None) -> tuple
     return int(allp[best, 1]), float(allp[best, 0])
 
 
+def best_candidate_device(local: torch.Tensor, global_offset: int, group=None) -> torch.Tensor:
+    """Same reduction as `best_candidate` without a host round trip (for timed loops): returns a
+    device tensor [best loglik, global index].  Every rank contributes (max, its global index);
+    one all-gather of 16 B per rank; the first maximal pair in rank order wins (lowest index)."""
+    v = torch.nan_to_num(local, nan=-float("inf"))
+    i = torch.argmax(v)
+    pair = torch.stack([v[i], (i + global_offset).to(torch.float64)])
+    world = dist.get_world_size(group)
+    allp = torch.empty(2 * world, dtype=torch.float64, device=local.device)
+    dist.all_gather_into_tensor(allp, pair, group=group)
+    allp = allp.view(world, 2)
+    r = torch.argmax(allp[:, 0])
+    return allp[r]
+
+
 def sharded_loglik(Theta: np.ndarray, evaluate: Callable[[np.ndarray], torch.Tensor], group=None,
                    device=None) -> GatherResult:
     """Evaluate Θ (P×B, identical on every rank) sharded over the group: rank r evaluates its
