@@ -168,9 +168,10 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   constexpr int CH = kTC * LDP;               // doubles per chunk
   constexpr int PER = (CH + kBlock - 1) / kBlock;
   constexpr int NZ = M - 1;                   // non-constant loading columns
-  constexpr bool USE_MFMA = (NZ == 2) && (NP <= 32);  // fragments + LDS scratch budget
+  constexpr bool USE_MFMA = (NZ == 2 || NZ == 4) && (NP <= 32);  // fragments + LDS scratch budget
   constexpr int NK = (NP + 3) / 4;            // MFMA k-steps (4 maturities each)
   constexpr int NRT = 64 * NZ / 16;           // MFMA row tiles per wave (16 (cand, col) pairs each)
+  constexpr int RGN = (NZ == 2) ? NRT : 4;    // row tiles accumulated at once (bounds live accumulators)
   constexpr int TB = 16;                      // steps per MFMA block
   constexpr int SS = 64 * NZ + 2;             // scratch row stride (doubles): one row per step
   constexpr int SCR = USE_MFMA ? (TB * SS) : 2;
@@ -293,8 +294,10 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
 #pragma unroll
     for (int i = 0; i < M; ++i)
 #pragma unroll
-      for (int j = 0; j < M; ++j) R[i][j] = sigma2 * 0.5 * (X[i][j] + X[j][i]);
+      for (int j = 0; j < M; ++j) R[i][j] = collapsed ? sigma2 * 0.5 * (X[i][j] + X[j][i]) : G[i][j];
   }
+  // From here R holds σ²(Z'Z)⁻¹ on collapsed lanes and G = Z'Z on capacitance lanes (one
+  // register image for both: each lane only ever needs one of them).
 
   double beta[M], Pm[M][M];
   const bool init_ok = init_state<M, LEAD>(p, beta, Pm);
@@ -390,21 +393,21 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
       double zy[M];
       zy[0] = (double)N * yb_c.x;
 #pragma unroll
-      for (int j = 1; j < M; ++j) zy[j] = fma(yb_c.x, G[j][0], zc[j - 1]);
+      for (int j = 1; j < M; ++j) zy[j] = fma(yb_c.x, R[j][0], zc[j - 1]);
       double u[M];
       double bgb = 0.0, bzy = 0.0;
 #pragma unroll
       for (int i = 0; i < M; ++i) {
         double g = 0.0;
 #pragma unroll
-        for (int j = 0; j < M; ++j) g = fma(G[i][j], beta[j], g);
+        for (int j = 0; j < M; ++j) g = fma(R[i][j], beta[j], g);
         u[i] = zy[i] - g;
         bgb = fma(beta[i], g, bgb);
         bzy = fma(beta[i], zy[i], bzy);
       }
       const double vv = fma(-2.0, bzy, meta_c.y) + bgb;
       double W[M][M];
-      Capacitance<M>::solve(Pm, G, sigma2, W, det);
+      Capacitance<M>::solve(Pm, R, sigma2, W, det);
 #pragma unroll
       for (int i = 0; i < M; ++i)
 #pragma unroll
@@ -460,41 +463,60 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   if constexpr (USE_MFMA) {
     double* scr = scratch[wave];
     for (int t0 = 0; t0 < nsteps; t0 += TB) {
-      // ---- z̃ for steps t0 .. t0+15 of all 64 candidates: 8·NK MFMAs ----
+      // ---- z̃ for steps t0 .. t0+15 of all 64 candidates: NRT·NK MFMAs ----
       const double* cb = col_of(t0);  // TB consecutive columns of one chunk
-      yfm_double4 acc[NRT];
-#pragma unroll
-      for (int r = 0; r < NRT; ++r) acc[r] = yfm_double4{0.0, 0.0, 0.0, 0.0};
+      double bvk[NK];
 #pragma unroll
       for (int kk = 0; kk < NK; ++kk) {
         const int m = 4 * kk + (lane >> 4);
-        const double bv = (m < NP) ? cb[(lane & 15) * LDP + m] : 0.0;  // B[k = m][col = step]
-#pragma unroll
-        for (int r = 0; r < NRT; ++r) acc[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(Af[r][kk], bv, acc[r], 0, 0, 0);
+        bvk[kk] = (m < NP) ? cb[(lane & 15) * LDP + m] : 0.0;  // B[k = m][col = step]
       }
-      // D[row = pair][col = step]: lane l holds step l & 15, pairs 16r + (l >> 4) + 4q
 #pragma unroll
-      for (int r = 0; r < NRT; ++r)
+      for (int r0 = 0; r0 < NRT; r0 += RGN) {
+        yfm_double4 acc[RGN];
 #pragma unroll
-        for (int q4 = 0; q4 < 4; ++q4) scr[(lane & 15) * SS + 16 * r + (lane >> 4) + 4 * q4] = acc[r][q4];
+        for (int r = 0; r < RGN; ++r) acc[r] = yfm_double4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kk = 0; kk < NK; ++kk)
+#pragma unroll
+          for (int r = 0; r < RGN; ++r)
+            acc[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(Af[r0 + r][kk], bvk[kk], acc[r], 0, 0, 0);
+        // D[row = pair][col = step]: lane l holds step l & 15, pairs 16r + (l >> 4) + 4q
+#pragma unroll
+        for (int r = 0; r < RGN; ++r)
+#pragma unroll
+          for (int q4 = 0; q4 < 4; ++q4)
+            scr[(lane & 15) * SS + 16 * (r0 + r) + (lane >> 4) + 4 * q4] = acc[r][q4];
+      }
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's scratch writes landed
       __builtin_amdgcn_wave_barrier();
       const int tend = min(TB, nsteps - t0);
       // step operands for tt are read one step ahead (hides the LDS latency at 1 wave/SIMD)
-      double2 z2 = *reinterpret_cast<const double2*>(scr + 2 * lane);  // pairs 2·lane, 2·lane+1
+      auto read_z = [&](int tt, double (&z)[NZ]) {  // this lane's pairs NZ·lane .. NZ·lane + NZ − 1
+        const double* sp = scr + tt * SS + NZ * lane;
+#pragma unroll
+        for (int j = 0; j < NZ; j += 2) {
+          const double2 v = *reinterpret_cast<const double2*>(sp + j);
+          z[j] = v.x;
+          z[j + 1] = v.y;
+        }
+      };
+      double zc[NZ];
+      read_z(0, zc);
       double2 yb = *reinterpret_cast<const double2*>(cb + NP);
       double2 meta = *reinterpret_cast<const double2*>(cb + NP + 2);
       for (int tt = 0; tt < tend; ++tt) {
         const int t = t0 + tt;
         const int tn = min(tt + 1, TB - 1);
-        const double2 z2n = *reinterpret_cast<const double2*>(scr + tn * SS + 2 * lane);
+        double zn[NZ];
+        read_z(tn, zn);
         const double2 ybn = *reinterpret_cast<const double2*>(cb + tn * LDP + NP);
         const double2 metan = *reinterpret_cast<const double2*>(cb + tn * LDP + NP + 2);
-        const double zc[NZ] = {z2.x, z2.y};
         do_step(t, zc, yb, meta);
         record(t);
         rotate(t);
-        z2 = z2n;
+#pragma unroll
+        for (int j = 0; j < NZ; ++j) zc[j] = zn[j];
         yb = ybn;
         meta = metan;
       }
