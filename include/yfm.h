@@ -102,6 +102,41 @@ int yfm_loglik_batch_device(yfm_ctx* ctx, int model_kind, int param_space, const
 int yfm_filter_states(yfm_ctx* ctx, int model_kind, int param_space, const double* theta, int P, int B,
                       const int* T_use, double* beta_out, double* P_out, double* loglik_out);
 
+/* Length L of base.gamma, the observation-driven parameters predict reports as
+ * `states` (kalmanbasemodel.jl:58): 1 for DNS (dns.jl:18) and TVλ (tvλdns.jl:19,
+ * never set, so zeros), 2 for the GNS5 extension. */
+int yfm_gamma_dim(int model_kind);
+
+/* Batched predict — replaces, per candidate b,
+ *   set_params!(model, θ_b); predict(model, hcat(Y[:, 1:T_b], fill(NaN, N, horizon-1)))
+ * (filter.jl:250-282 on the NaN padding of forecasting.jl:141/161/242); horizon = 1
+ * is predict(model, Y[:, 1:T_b]).  T_b = T_use[b] (or T when T_use is NULL).
+ * Outputs, column-major with ncol = T + horizon - 1 columns per candidate (candidate
+ * b's columns beyond T_b + horizon - 1 are NaN):
+ *   preds N×ncol×B (preds[:, j] = ŷ for observation j+1), factors M×ncol×B,
+ *   states L×ncol×B (L = yfm_gamma_dim), loadings_1 / loadings_2 N×ncol×B (Z[:,2],
+ *   Z[:,3]; either may be NULL).  A candidate whose initialize_filter would throw
+ *   gets NaN everywhere.  Synchronous. */
+int yfm_predict(yfm_ctx* ctx, int model_kind, int param_space, const double* theta, int P, int B, const int* T_use,
+                int horizon, double* preds, double* factors, double* states, double* loadings_1,
+                double* loadings_2);
+
+/* Forecast blocks of the rolling-window driver (forecasting.jl:236-250):
+ *   res = vcat(factors[:, end-h+1:end], states[:, end-h+1:end], preds[:, end-h+1:end])
+ * of the predict call above, h = horizon.  out: (M+L+N) × h × B column-major.  This
+ * is the per-task record run_forecast_window_database stores (forecasting.jl:181-184). */
+int yfm_forecast(yfm_ctx* ctx, int model_kind, int param_space, const double* theta, int P, int B, const int* T_use,
+                 int horizon, double* out);
+
+/* Batched get_loss_array(model, Y[:, 1:T_b]; K) (filter.jl:211-247): mse_out (T-1)×B,
+ * column b holds the T_b - 1 per-step values -‖y_t - ŷ_t‖²/N/K (entry 1 is 0, as in
+ * the reference) followed by NaN.  A candidate for which the reference returns the
+ * scalar -Inf (a non-finite step) gets -Inf in all its entries; NaN where
+ * initialize_filter would throw.  K > 1 passes continue the filter state, as in the
+ * reference; K > 1 requires T_use = NULL.  Synchronous. */
+int yfm_loss_array(yfm_ctx* ctx, int model_kind, int param_space, const double* theta, int P, int B,
+                   const int* T_use, int K, double* mse_out);
+
 /* Counters of the last completed batch on this ctx: candidates where the
  * reference would have thrown (NaN outputs) and candidates returning -Inf.
  * For yfm_loglik_batch_device, synchronise the stream first. */

@@ -219,3 +219,83 @@ def loglik_ld_tvl(maturities, Y, Theta, space: int = 0, T_use=None, dtype=LD) ->
     ll[neg | ~np.isfinite(ll)] = -np.inf
     ll[throws] = np.nan
     return ll
+
+
+def predict_traj_tvl(maturities, Y, Theta_c, horizon: int = 1, T_use=None, dtype=LD) -> np.ndarray:
+    """TVλ state trajectory of predict (filter.jl:250-282) on hcat(Y[:, 1:T_b], NaN × (horizon−1))
+    in `dtype` arithmetic (capacitance form, as loglik_ld_tvl): returns A (B, T + horizon, 4),
+    A[b, j] = β after filter! step j + 1 (the final NaN step included), NaN past candidate b's
+    T_b + horizon steps.  Used as the truth proxy (long double) and as a second FP64 restatement
+    (dtype = float64) for the noise floor of ill-conditioned EKF runs."""
+    from .kalman_oracle import KIND_TVL, transform_codes  # noqa: F401
+    M = 4
+    Theta_c = np.asarray(Theta_c, dtype=np.float64)
+    B = Theta_c.shape[1]
+    tc = Theta_c.astype(dtype)
+    sig2 = tc[0]
+    k = 1
+    U = np.zeros((B, M, M), dtype)
+    for j in range(M):
+        for i in range(j + 1):
+            U[:, i, j] = tc[k]
+            k += 1
+    Q = np.einsum("bli,blj->bij", U, U)
+    d = tc[k:k + M].T.copy()
+    k += M
+    Phi = tc[k:k + M * M].T.reshape(B, M, M).copy()
+    mats = np.asarray(maturities, dtype=np.float64).astype(dtype)
+    N = len(mats)
+    I = np.eye(M, dtype=dtype)
+    beta, _ = _gesv(I - Phi, d[..., None])
+    beta = beta[..., 0]
+    K2 = np.eye(M * M, dtype=dtype)[None] - np.einsum("bij,bkl->bikjl", Phi, Phi).reshape(B, M * M, M * M)
+    vq = np.transpose(Q, (0, 2, 1)).reshape(B, M * M)
+    vp, _ = _gesv(K2, vq[..., None])
+    P = np.transpose(vp[..., 0].reshape(B, M, M), (0, 2, 1))
+    Y = np.asarray(Y, dtype=np.float64).astype(dtype)
+    T = Y.shape[1]
+    nobs = np.full(B, T) if T_use is None else np.asarray(T_use)
+    steps = nobs + horizon
+    A = np.full((B, T + horizon, M), np.nan)
+    Z = np.ones((B, N, M), dtype)
+    with np.errstate(all="ignore"):
+        for t in range(int(steps.max())):
+            act = t < steps
+            col = Y[:, t] if t < T else np.full(N, np.nan, dtype)
+            nan = (t >= nobs) | bool(np.isnan(col).any())
+            beta_p = d + np.einsum("bij,bj->bi", Phi, beta)
+            P_p = Phi @ P @ np.transpose(Phi, (0, 2, 1)) + Q
+            lam = dtype(0.01) + np.exp(beta[:, 3])
+            tau = lam[:, None] * mats[None, :]
+            z = np.exp(-tau)
+            Z[:, :, 1] = (1 - z) / tau
+            Z[:, :, 2] = Z[:, :, 1] - z
+            dl = lam - dtype(0.01)
+            dz1 = z / lam[:, None] - z / (lam[:, None] ** 2 * mats[None, :])
+            dz2 = mats[None, :] * z
+            Z[:, :, 3] = ((beta[:, 1] + beta[:, 2])[:, None] * dz1 + beta[:, 2][:, None] * dz2) * dl[:, None]
+            r = np.nan_to_num(col)[None, :] - np.einsum("bni,bi->bn", Z[:, :, :3], beta[:, :3])
+            u = np.einsum("bni,bn->bi", Z, r)
+            G = np.einsum("bni,bnj->bij", Z, Z)
+            W, det = _gesv(sig2[:, None, None] * I + P @ G, P)
+            W = (W + np.transpose(W, (0, 2, 1))) / 2
+            kv = np.einsum("bij,bj->bi", W, u)
+            beta_u = d + np.einsum("bij,bj->bi", Phi, beta + kv)
+            P_u = sig2[:, None, None] * (Phi @ W @ np.transpose(Phi, (0, 2, 1))) + Q
+            upd = act & ~nan & (det != 0)
+            prd = act & nan
+            beta = np.where(upd[:, None], beta_u, np.where(prd[:, None], beta_p, beta))
+            P = np.where(upd[:, None, None], P_u, np.where(prd[:, None, None], P_p, P))
+            A[act, t] = beta[act].astype(np.float64)
+    return A
+
+
+def fitted_tvl(maturities, A):
+    """ŷ = Z(β₄)[:, 1:3] β[1:3] for states A (..., 4) (filter.jl:15/:33, tvλdns.jl:53-64): (..., N)."""
+    m = np.asarray(maturities, dtype=A.dtype)
+    with np.errstate(all="ignore"):
+        lam = 0.01 + np.exp(A[..., 3:4])
+        tau = lam * m
+        z = np.exp(-tau)
+        s = (1 - z) / tau
+        return A[..., 0:1] + s * A[..., 1:2] + (s - z) * A[..., 2:3]

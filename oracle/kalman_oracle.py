@@ -312,7 +312,7 @@ def set_params(s: KalmanState, params):
         set_params_base(s, params[1:])
         dns_loadings(params[0], s.maturities, s.Z)
     elif s.kind == KIND_GNS:
-        s.gamma = np.array([params[0]])
+        s.gamma = np.array(params[0:2])  # L = 2 (both γ) for the extension
         set_params_base(s, params[2:])
         gns_loadings(params[0:2], s.maturities, s.Z)
     elif s.kind == KIND_TVL:
@@ -454,19 +454,23 @@ def loglik(kind, maturities, M, data, theta, space=0, record=None):
 
 
 def get_loss_array(s: KalmanState, data, K: int = 1):
-    """filter.jl:211-247 with K=1 (the only value the driver uses, YieldFactorModels.jl:318)."""
+    """filter.jl:211-247.  The K passes continue the filter state (initialize_filter runs once,
+    :214); the set_params!(catched_params) of passes k > 1 (:223-225) re-sets the same flat
+    parameters of a Kalman model (get_params returns flat_params, paramoperations.jl:1-4), so it
+    changes nothing and is omitted.  Returns the scalar -Inf where the reference does (:234-236)."""
     data = np.asarray(data, dtype=np.float64)
     nobs = data.shape[1]
     initialize_filter(s)
     mse = np.zeros(nobs - 1)
     with np.errstate(all="ignore"):
-        for t in range(1, nobs):
-            filter_step(s, data[:, t - 1].copy())
-            s.v = data[:, t - 1] - s.y_pred
-            if t > 1:
-                mse[t - 1] -= float(s.v @ s.v)
-            if not np.isfinite(mse[t - 1]):
-                return -math.inf
+        for _k in range(K):
+            for t in range(1, nobs):
+                filter_step(s, data[:, t - 1].copy())
+                s.v = data[:, t - 1] - s.y_pred
+                if t > 1:
+                    mse[t - 1] -= float(s.v @ s.v)
+                if not np.isfinite(mse[t - 1]):
+                    return -math.inf
     return mse / s.N / K
 
 
@@ -477,7 +481,7 @@ def predict(s: KalmanState, data):
     initialize_filter(s)
     preds = np.empty((N, nobs))
     factors = np.empty((s.M, nobs))
-    states = np.empty((1, nobs))
+    states = np.empty((len(s.gamma), nobs))
     fl1 = np.empty((N, nobs))
     fl2 = np.empty((N, nobs))
     with np.errstate(all="ignore"):
@@ -497,3 +501,15 @@ def predict(s: KalmanState, data):
     fl2[:, -1] = s.Z[:, 2]
     return dict(preds=preds, factors=factors, states=states,
                 factor_loadings_1=fl1, factor_loadings_2=fl2)
+
+
+def pad_nan(data, horizon: int):
+    """hcat(data, fill(NaN, N, horizon-1)) — the forecast padding of forecasting.jl:141, :161, :242."""
+    data = np.asarray(data, dtype=np.float64)
+    return np.hstack([data, np.full((data.shape[0], horizon - 1), np.nan)])
+
+
+def forecast_block(s: KalmanState, data, horizon: int):
+    """forecasting.jl:242-247: vcat(factors, states, preds)[:, end-h+1:end] of predict on the padded data."""
+    r = predict(s, pad_nan(data, horizon))
+    return np.vstack([r["factors"][:, -horizon:], r["states"][:, -horizon:], r["preds"][:, -horizon:]])

@@ -154,3 +154,63 @@ def test_c_oracle_headline_batch(coracle):
     out = coracle(KIND_DNS, Y, S.maturities_30(), Th)
     ref = [O.loglik(KIND_DNS, S.maturities_30(), 3, Y, Th[:, b]) for b in range(8)]
     assert rel_err(out, ref) <= 1e-11
+
+
+# ---- §8(f) trajectory outputs: predict, forecast blocks, get_loss_array ----------------
+TRAJ = sorted(p.stem for p in (ROOT / "tests" / "golden" / "traj").glob("*.npz"))
+
+
+def _traj(name):
+    with np.load(ROOT / "tests" / "golden" / "traj" / f"{name}.npz", allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def _state(kind, mats, theta_c):
+    from yfm_amd.params import state_dim
+    s = O.KalmanState.fresh(kind, mats, state_dim(kind))
+    O.set_params(s, theta_c)
+    return s
+
+
+@pytest.mark.parametrize("name", TRAJ)
+def test_traj_golden_numpy_oracle_reproduces(name):
+    """The committed trajectory fixtures are the oracle's outputs (generator: tests/golden/traj)."""
+    g = _traj(name)
+    kind, h = int(g["kind"]), int(g["horizon"])
+    for b in range(g["Theta"].shape[1]):
+        Tb = int(g["T_use"][b])
+        r = O.predict(_state(kind, g["maturities"], g["Theta"][:, b]), O.pad_nan(g["Y"][:, :Tb], h))
+        for k, v in r.items():
+            np.testing.assert_array_equal(v, g[f"predict_{k}"][:, :Tb + h - 1, b])
+        la = O.get_loss_array(_state(kind, g["maturities"], g["Theta"][:, b]), g["Y"], K=2)
+        np.testing.assert_array_equal(la, g["loss_array_K2"][:, b])
+
+
+def test_predict_alignment_and_loss_array_consistency():
+    """Two independent readings of filter.jl: get_loss_array's residual at Julia step t ≥ 2 is
+    y_t − preds[:, t−1] of predict (filter.jl:228 vs :265), and preds[:, j] = Z·factors[:, j−1]."""
+    from yfm_amd.params import KIND_DNS
+    mats = S.maturities_30()
+    Y = S.simulate_panel(KIND_DNS, 600)[:, :50]
+    th = S.theta0_constrained(KIND_DNS)
+    r = O.predict(_state(KIND_DNS, mats, th), Y)
+    la = O.get_loss_array(_state(KIND_DNS, mats, th), Y)
+    resid = Y[:, 1:49] - r["preds"][:, :48]  # Julia t = 2..49 ↔ preds[:, t-1]
+    np.testing.assert_allclose(la[1:], -(resid ** 2).sum(axis=0) / 30, rtol=1e-12)
+    assert la[0] == 0.0
+    Z = np.ones((30, 3))
+    O.dns_loadings(th[0], mats, Z)
+    np.testing.assert_allclose(r["preds"][:, 1:], Z @ r["factors"][:, :-1], rtol=1e-12, atol=1e-12)
+
+
+def test_loss_array_passes_continue_the_state():
+    """K = 2 passes (filter.jl:221-242) do not re-initialise: pass 2 equals a single pass over the
+    panel [Y[:, 1:T-1], Y] read from the second copy on."""
+    from yfm_amd.params import KIND_DNS
+    mats = S.maturities_30()
+    Y = S.simulate_panel(KIND_DNS, 600)[:, :30]
+    th = S.theta0_constrained(KIND_DNS)
+    two = O.get_loss_array(_state(KIND_DNS, mats, th), Y, K=2)
+    Yt = np.hstack([Y[:, :29], Y])
+    one = O.get_loss_array(_state(KIND_DNS, mats, th), Yt, K=1)
+    np.testing.assert_allclose(2 * two, one[:29] + np.concatenate([[0.0], one[30:]]), rtol=1e-12)

@@ -39,6 +39,8 @@ int set_error(int code, const char* fmt, ...) {
 
 int state_dim(int kind) { return kind == YFM_MODEL_DNS ? 3 : kind == YFM_MODEL_TVL ? 4 : kind == YFM_MODEL_GNS5 ? 5 : -1; }
 int n_lead(int kind) { return kind == YFM_MODEL_DNS ? 1 : kind == YFM_MODEL_TVL ? 0 : 2; }
+// L = length of base.gamma (kalmanbasemodel.jl:58): DNS 1 (dns.jl:18), TVλ 1 (tvλdns.jl:19, never set), GNS5 2
+int gamma_dim(int kind) { return kind == YFM_MODEL_GNS5 ? 2 : (state_dim(kind) < 0 ? -1 : 1); }
 int param_count(int kind) {
   const int M = state_dim(kind);
   if (M < 0) return -1;
@@ -76,6 +78,8 @@ struct yfm_ctx {
   DevBuf theta, out, tuse, rec_beta, rec_P;
   DevBuf flags;  // 2 × unsigned int
   DevBuf scratch;  // per-candidate work records (TVλ init)
+  DevBuf traj, init_bad;       // trajectory-mode state records, per-candidate init-throw marks
+  DevBuf tiled_raw, tiled_panel;  // get_loss_array with K > 1 passes: the panel tiled K times
   // TVλ maturity-jump tables, one per lane count L = 2^l (built lazily, reset by set_panel)
   std::vector<double> mats_host;
   int gap_K[7] = {-1, -1, -1, -1, -1, -1, -1};
@@ -153,8 +157,16 @@ int tvl_gaps(yfm_ctx* ctx, int L, yfm::TvlGaps& g) {
   return YFM_OK;
 }
 
+// A panel other than the context's (get_loss_array's K-times tiled panel).
+struct PanelView {
+  const double* raw;
+  const double* panel;
+  int T;
+};
+
 int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int B, const int* d_T_use,
-           double* d_out, double* d_rb, double* d_rP, hipStream_t s) {
+           double* d_out, double* d_rb, double* d_rP, hipStream_t s, int horizon = 0, int rec_len = 0,
+           const PanelView* pv = nullptr) {
   YFM_HIP_CHECK(hipMemsetAsync(ctx->flags.p, 0, 2 * sizeof(unsigned int), s));
   if (B == 0) return YFM_OK;
   yfm::LaunchArgs a;
@@ -175,6 +187,13 @@ int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int 
   a.rec_beta = d_rb;
   a.rec_P = d_rP;
   a.scratch = nullptr;
+  a.horizon = horizon;
+  a.rec_len = d_rb ? (rec_len > 0 ? rec_len : ctx->T - 1) : 0;
+  if (pv) {
+    a.raw = pv->raw;
+    a.panel = pv->panel;
+    a.T = pv->T;
+  }
   a.stream = s;
   hipError_t e;
   if (kind == YFM_MODEL_TVL) {
@@ -193,6 +212,64 @@ int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int 
   }
   if (e != hipSuccess) return set_error(YFM_EHIP, "kernel launch: %s", hipGetErrorString(e));
   return YFM_OK;
+}
+
+// Upload θ (and T_use) for a host-pointer call; returns the device pointers.
+int stage_inputs(yfm_ctx* ctx, const double* theta, int P, int B, const int* T_use, const double** d_th,
+                 const int** d_tu) {
+  const size_t nb = (size_t)(B > 0 ? B : 1);
+  YFM_HIP_CHECK(ctx->theta.ensure(sizeof(double) * (size_t)P * nb));
+  YFM_HIP_CHECK(ctx->out.ensure(sizeof(double) * nb));
+  if (B > 0)
+    YFM_HIP_CHECK(hipMemcpyAsync(ctx->theta.p, theta, sizeof(double) * (size_t)P * B, hipMemcpyHostToDevice,
+                                 ctx->stream));
+  *d_th = static_cast<const double*>(ctx->theta.p);
+  *d_tu = nullptr;
+  if (T_use && B > 0) {
+    YFM_HIP_CHECK(ctx->tuse.ensure(sizeof(int) * nb));
+    YFM_HIP_CHECK(hipMemcpyAsync(ctx->tuse.p, T_use, sizeof(int) * B, hipMemcpyHostToDevice, ctx->stream));
+    *d_tu = static_cast<const int*>(ctx->tuse.p);
+  }
+  return YFM_OK;
+}
+
+// Trajectory mode: run the filter kernel recording the last rec_len states of every
+// candidate into ctx->traj and mark the candidates whose initialize_filter threw.
+int run_trajectory(yfm_ctx* ctx, int kind, int space, const double* d_th, int P, int B, const int* d_tu,
+                   int horizon, int rec_len, const PanelView* pv = nullptr) {
+  const int M = state_dim(kind);
+  const size_t n = (size_t)B * rec_len * M;
+  YFM_HIP_CHECK(ctx->traj.ensure(sizeof(double) * (n > 0 ? n : 1)));
+  YFM_HIP_CHECK(ctx->init_bad.ensure((size_t)(B > 0 ? B : 1)));
+  YFM_HIP_CHECK(hipMemsetAsync(ctx->traj.p, 0xff, sizeof(double) * n, ctx->stream));  // NaN fill
+  if (int r = launch(ctx, kind, space, d_th, P, B, d_tu, static_cast<double*>(ctx->out.p),
+                     static_cast<double*>(ctx->traj.p), nullptr, ctx->stream, horizon, rec_len, pv))
+    return r;
+  YFM_HIP_CHECK(yfm::launch_init_bad(static_cast<const double*>(ctx->out.p), B,
+                                     static_cast<unsigned char*>(ctx->init_bad.p), ctx->stream));
+  return YFM_OK;
+}
+
+yfm::PredictArgs predict_args(yfm_ctx* ctx, int kind, const double* d_th, int P, int B, const int* d_tu,
+                              int horizon, int rec_len) {
+  yfm::PredictArgs a{};
+  a.kind = kind;
+  a.M = state_dim(kind);
+  a.L = gamma_dim(kind);
+  a.N = ctx->N;
+  a.P = P;
+  a.B = B;
+  a.T = ctx->T;
+  a.horizon = horizon;
+  a.ncol = ctx->T + horizon - 1;
+  a.theta = d_th;
+  a.mats = static_cast<const double*>(ctx->mats.p);
+  a.T_use = d_tu;
+  a.rec = static_cast<const double*>(ctx->traj.p);
+  a.rec_len = rec_len;
+  a.init_bad = static_cast<const unsigned char*>(ctx->init_bad.p);
+  a.stream = ctx->stream;
+  return a;
 }
 
 int validate_tuse(const int* T_use, int B, int T) {
@@ -246,6 +323,7 @@ void yfm_destroy(yfm_ctx* ctx) {
   for (DevBuf* b : {&ctx->panel, &ctx->mats, &ctx->raw, &ctx->theta, &ctx->out, &ctx->tuse, &ctx->rec_beta,
                     &ctx->rec_P, &ctx->flags, &ctx->scratch})
     b->release();
+  for (DevBuf* b : {&ctx->traj, &ctx->init_bad, &ctx->tiled_raw, &ctx->tiled_panel}) b->release();
   for (DevBuf& b : ctx->gap_buf) b.release();
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -338,7 +416,7 @@ int yfm_filter_states(yfm_ctx* ctx, int model_kind, int param_space, const doubl
   }
   if (int r = launch(ctx, model_kind, param_space, static_cast<const double*>(ctx->theta.p), P, B, d_tuse,
                      static_cast<double*>(ctx->out.p), static_cast<double*>(ctx->rec_beta.p),
-                     static_cast<double*>(ctx->rec_P.p), ctx->stream))
+                     static_cast<double*>(ctx->rec_P.p), ctx->stream, 0, ctx->T - 1))
     return r;
   YFM_HIP_CHECK(hipMemcpyAsync(loglik_out, ctx->out.p, sizeof(double) * B, hipMemcpyDeviceToHost, ctx->stream));
   YFM_HIP_CHECK(hipMemcpyAsync(beta_out, ctx->rec_beta.p, sizeof(double) * steps * M, hipMemcpyDeviceToHost,
@@ -355,6 +433,112 @@ int yfm_last_batch_flags(yfm_ctx* ctx, long long* n_init_throw, long long* n_neg
   YFM_HIP_CHECK(hipMemcpy(h, ctx->flags.p, sizeof(h), hipMemcpyDeviceToHost));
   if (n_init_throw) *n_init_throw = h[0];
   if (n_neg_inf) *n_neg_inf = h[1];
+  return YFM_OK;
+}
+
+int yfm_gamma_dim(int model_kind) { return gamma_dim(model_kind); }
+
+int yfm_predict(yfm_ctx* ctx, int model_kind, int param_space, const double* theta, int P, int B, const int* T_use,
+                int horizon, double* preds, double* factors, double* states, double* loadings_1,
+                double* loadings_2) {
+  if (int r = check_ctx(ctx)) return r;
+  if (int r = check_batch(ctx, model_kind, param_space, P, B)) return r;
+  if (horizon < 1) return set_error(YFM_EINVAL, "horizon = %d < 1", horizon);
+  if (B > 0 && (!theta || !preds || !factors || !states)) return set_error(YFM_EINVAL, "null pointer argument");
+  if (int r = validate_tuse(T_use, B, ctx->T)) return r;
+  if (B == 0) return YFM_OK;
+  const int M = state_dim(model_kind), L = gamma_dim(model_kind), N = ctx->N;
+  const int rec_len = ctx->T + horizon;  // every step of the longest candidate
+  const size_t ncol = (size_t)ctx->T + horizon - 1;
+  const double* d_th;
+  const int* d_tu;
+  if (int r = stage_inputs(ctx, theta, P, B, T_use, &d_th, &d_tu)) return r;
+  if (int r = run_trajectory(ctx, model_kind, param_space, d_th, P, B, d_tu, horizon, rec_len)) return r;
+  // outputs: one device block [preds | load1 | load2 | factors | states]
+  const size_t nN = (size_t)N * ncol * B, nM = (size_t)M * ncol * B, nL = (size_t)L * ncol * B;
+  YFM_HIP_CHECK(ctx->rec_P.ensure(sizeof(double) * (3 * nN + nM + nL)));
+  double* d = static_cast<double*>(ctx->rec_P.p);
+  yfm::PredictArgs a = predict_args(ctx, model_kind, d_th, P, B, d_tu, horizon, rec_len);
+  a.preds = d;
+  a.load1 = loadings_1 ? d + nN : nullptr;
+  a.load2 = loadings_2 ? d + 2 * nN : nullptr;
+  a.factors = d + 3 * nN;
+  a.states = d + 3 * nN + nM;
+  YFM_HIP_CHECK(yfm::launch_predict_emit(a));
+  YFM_HIP_CHECK(hipMemcpyAsync(preds, a.preds, sizeof(double) * nN, hipMemcpyDeviceToHost, ctx->stream));
+  if (loadings_1)
+    YFM_HIP_CHECK(hipMemcpyAsync(loadings_1, a.load1, sizeof(double) * nN, hipMemcpyDeviceToHost, ctx->stream));
+  if (loadings_2)
+    YFM_HIP_CHECK(hipMemcpyAsync(loadings_2, a.load2, sizeof(double) * nN, hipMemcpyDeviceToHost, ctx->stream));
+  YFM_HIP_CHECK(hipMemcpyAsync(factors, a.factors, sizeof(double) * nM, hipMemcpyDeviceToHost, ctx->stream));
+  YFM_HIP_CHECK(hipMemcpyAsync(states, a.states, sizeof(double) * nL, hipMemcpyDeviceToHost, ctx->stream));
+  YFM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+  return YFM_OK;
+}
+
+int yfm_forecast(yfm_ctx* ctx, int model_kind, int param_space, const double* theta, int P, int B, const int* T_use,
+                 int horizon, double* out) {
+  if (int r = check_ctx(ctx)) return r;
+  if (int r = check_batch(ctx, model_kind, param_space, P, B)) return r;
+  if (horizon < 1) return set_error(YFM_EINVAL, "horizon = %d < 1", horizon);
+  if (B > 0 && (!theta || !out)) return set_error(YFM_EINVAL, "null pointer argument");
+  if (int r = validate_tuse(T_use, B, ctx->T)) return r;
+  if (B == 0) return YFM_OK;
+  const int M = state_dim(model_kind), L = gamma_dim(model_kind), N = ctx->N;
+  const double* d_th;
+  const int* d_tu;
+  if (int r = stage_inputs(ctx, theta, P, B, T_use, &d_th, &d_tu)) return r;
+  if (int r = run_trajectory(ctx, model_kind, param_space, d_th, P, B, d_tu, horizon, horizon + 1)) return r;
+  const size_t n = (size_t)(M + L + N) * horizon * B;
+  YFM_HIP_CHECK(ctx->rec_P.ensure(sizeof(double) * n));
+  yfm::PredictArgs a = predict_args(ctx, model_kind, d_th, P, B, d_tu, horizon, horizon + 1);
+  a.preds = static_cast<double*>(ctx->rec_P.p);
+  YFM_HIP_CHECK(yfm::launch_forecast_emit(a));
+  YFM_HIP_CHECK(hipMemcpyAsync(out, a.preds, sizeof(double) * n, hipMemcpyDeviceToHost, ctx->stream));
+  YFM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+  return YFM_OK;
+}
+
+int yfm_loss_array(yfm_ctx* ctx, int model_kind, int param_space, const double* theta, int P, int B,
+                   const int* T_use, int K, double* mse_out) {
+  if (int r = check_ctx(ctx)) return r;
+  if (int r = check_batch(ctx, model_kind, param_space, P, B)) return r;
+  if (K < 1) return set_error(YFM_EINVAL, "K = %d < 1", K);
+  if (K > 1 && T_use) return set_error(YFM_EUNSUPPORTED, "K > 1 passes with per-candidate windows");
+  if (B > 0 && (!theta || !mse_out)) return set_error(YFM_EINVAL, "null pointer argument");
+  if (int r = validate_tuse(T_use, B, ctx->T)) return r;
+  const int T1 = ctx->T - 1;
+  if (B == 0 || T1 <= 0) return YFM_OK;
+  const double* d_th;
+  const int* d_tu;
+  if (int r = stage_inputs(ctx, theta, P, B, T_use, &d_th, &d_tu)) return r;
+  PanelView pv{static_cast<const double*>(ctx->raw.p), static_cast<const double*>(ctx->panel.p), ctx->T};
+  if (K > 1) {
+    // the K passes continue the filter state (filter.jl:221-242 never re-initialises):
+    // filter the panel [Y[:, 1:T−1] × K, Y[:, T]] once
+    const int Tk = K * T1 + 1;
+    const size_t colb = sizeof(double) * ctx->N;
+    YFM_HIP_CHECK(ctx->tiled_raw.ensure(colb * Tk));
+    YFM_HIP_CHECK(ctx->tiled_panel.ensure(sizeof(double) * (size_t)ctx->ldp * Tk));
+    char* dst = static_cast<char*>(ctx->tiled_raw.p);
+    for (int k = 0; k < K; ++k)
+      YFM_HIP_CHECK(hipMemcpyAsync(dst + colb * k * T1, ctx->raw.p, colb * T1, hipMemcpyDeviceToDevice, ctx->stream));
+    YFM_HIP_CHECK(hipMemcpyAsync(dst + colb * K * T1, static_cast<char*>(ctx->raw.p) + colb * T1, colb,
+                                 hipMemcpyDeviceToDevice, ctx->stream));
+    YFM_HIP_CHECK(yfm::launch_prep_panel(static_cast<const double*>(ctx->tiled_raw.p), ctx->N, Tk, ctx->np, ctx->ldp,
+                                         static_cast<double*>(ctx->tiled_panel.p), ctx->stream));
+    pv = PanelView{static_cast<const double*>(ctx->tiled_raw.p), static_cast<const double*>(ctx->tiled_panel.p), Tk};
+  }
+  const int rec_len = pv.T - 1;
+  if (int r = run_trajectory(ctx, model_kind, param_space, d_th, P, B, d_tu, 0, rec_len, &pv)) return r;
+  YFM_HIP_CHECK(hipMemsetAsync(ctx->flags.p, 0, 2 * sizeof(unsigned int), ctx->stream));
+  YFM_HIP_CHECK(ctx->rec_P.ensure(sizeof(double) * (size_t)T1 * B));
+  yfm::PredictArgs a = predict_args(ctx, model_kind, d_th, P, B, d_tu, 1, rec_len);
+  a.preds = static_cast<double*>(ctx->rec_P.p);
+  YFM_HIP_CHECK(yfm::launch_loss_array(a, static_cast<const double*>(ctx->raw.p), T1, K,
+                                       static_cast<unsigned int*>(ctx->flags.p)));
+  YFM_HIP_CHECK(hipMemcpyAsync(mse_out, a.preds, sizeof(double) * (size_t)T1 * B, hipMemcpyDeviceToHost, ctx->stream));
+  YFM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
   return YFM_OK;
 }
 

@@ -17,6 +17,8 @@ struct LaunchArgs {
   double* rec_beta;     // optional trajectories
   double* rec_P;
   double* scratch;      // per-candidate work records (tvl_scratch_bytes)
+  int horizon = 0;      // 0: loglik mode; ≥ 1: trajectory mode (predict / forecast / loss array)
+  int rec_len = 0;      // recorded steps per candidate (the last rec_len), stride of rec_beta / rec_P
   hipStream_t stream;
 };
 
@@ -37,6 +39,28 @@ struct TvlGaps {
   const int* idx = nullptr;   // device, N
 };
 hipError_t launch_tvl(const LaunchArgs& a, const TvlGaps& g, int lanes);
+// Trajectory outputs (yfm_predict.hip) from a recorded state trajectory.
+struct PredictArgs {
+  int kind, M, L, N, P, B, T;
+  int ncol;                  // predict: output columns per candidate (T + horizon − 1)
+  int horizon;
+  const double* theta;       // P×B device
+  const double* mats;        // N device
+  const int* T_use;          // B device or nullptr
+  const double* rec;         // M × rec_len × B trajectory (yfm_kernels.hip / yfm_tvl.hip)
+  int rec_len;
+  const unsigned char* init_bad;  // B: initialize_filter threw
+  double* preds;             // predict: N×ncol×B; forecast: (M+L+N)×h×B; loss array: (T−1)×B
+  double* factors;           // predict: M×ncol×B
+  double* states;            // predict: L×ncol×B
+  double* load1;             // predict: N×ncol×B or nullptr
+  double* load2;
+  hipStream_t stream;
+};
+hipError_t launch_init_bad(const double* ll, int B, unsigned char* bad, hipStream_t s);
+hipError_t launch_predict_emit(const PredictArgs& a);
+hipError_t launch_forecast_emit(const PredictArgs& a);
+hipError_t launch_loss_array(const PredictArgs& a, const double* Y, int T1, int passes, unsigned int* flags);
 hipError_t launch_prep_panel(const double* Y, int N, int T, int np, int ldp, double* out, hipStream_t s);
 
 }  // namespace yfm

@@ -163,7 +163,8 @@ template <int NP, int M, int LEAD, bool RECORD>
 __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     const double* __restrict__ theta, int P, int B, int space, const double* __restrict__ panel, int T, int N,
     const double* __restrict__ mats, const int* __restrict__ T_use, double* __restrict__ out,
-    unsigned int* __restrict__ flags, double* __restrict__ rec_beta, double* __restrict__ rec_P) {
+    unsigned int* __restrict__ flags, double* __restrict__ rec_beta, double* __restrict__ rec_P, int horizon,
+    int rec_len) {
   constexpr int LDP = NP + 4;
   constexpr int CH = kTC * LDP;               // doubles per chunk
   constexpr int PER = (CH + kBlock - 1) / kBlock;
@@ -192,7 +193,12 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
 
   if (tid == 0) s_nobs_max = 0;
   __syncthreads();
-  atomicMax(&s_nobs_max, live ? nobs : 0);
+  // loglik mode (horizon = 0): filter! over columns 0 .. nobs−2 (filter.jl:190).  Trajectory
+  // mode (horizon ≥ 1, predict, filter.jl:250-282): columns 0 .. nobs−1, then horizon NaN
+  // steps (the NaN padding of forecasting.jl:141 plus predict's final NaN step).
+  const int my_steps = horizon > 0 ? nobs + horizon : nobs - 1;
+  const int my_data = horizon > 0 ? nobs : nobs - 1;  // steps t < my_data read column t
+  atomicMax(&s_nobs_max, live ? my_steps : 0);
 
   // ---- decode θ_b, loadings, Z'Z, initial state ----------------------------------
   Params<M, LEAD> p;
@@ -306,17 +312,16 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   double sumq = 0.0;
   bool neg = false;
   double last_det = 0.0, last_q = 0.0;  // fresh model: F = 0, F⁻¹ = 0, v = 0 (kalmanbasemodel.jl:65-67)
-  const int my_steps = nobs - 1;
 
   // wave-uniform facts for the fast path
-  int wmin = live ? my_steps : 0x7fffffff;
+  int wmin = live ? my_data : 0x7fffffff;
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) wmin = min(wmin, __shfl_xor(wmin, off));
-  const int wave_min_steps = __builtin_amdgcn_readfirstlane(wmin);
+  const int wave_min_data = __builtin_amdgcn_readfirstlane(wmin);
   const bool wave_all_collapsed = __ballot(!collapsed) == 0ull;
 
   __syncthreads();
-  const int nsteps = max(s_nobs_max - 1, 0);
+  const int nsteps = max(s_nobs_max, 0);
 
   // ---- panel staging: LDS holds chunks c and c+1 while chunk c is processed ----------
   double pre[PER];
@@ -349,11 +354,12 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
 
   // one filter step given z̃_t (zc), (ȳ, ỹ'ỹ) and (nanflag, y'y) of column t
   auto do_step = [&](int t, const double (&zc)[NZ], double2 yb_c, double2 meta_c) {
-    const bool fast = (t >= 1) && (meta_c.x == 0.0) && (t < wave_min_steps) && wave_all_collapsed;
+    const bool fast = (t >= 1) && (meta_c.x == 0.0) && (t < wave_min_data) && wave_all_collapsed;
     if (fast) {
       double bf[M], Pf[M][M], det, q;
       collapsed_update<M>(zc, yb_c.x, yb_c.y, R, rsig2, beta, Pm, bf, Pf, det, q);
-      propagate_state<M, LEAD>(p, bf, Pf, beta, Pm);
+      // (a singular F at t ≥ 2 makes the loglik −Inf whatever the state; trajectories skip the update)
+      if (!RECORD || det != 0.0) propagate_state<M, LEAD>(p, bf, Pf, beta, Pm);
       last_det = det;
       last_q = q;
       ld.mul(det);
@@ -364,7 +370,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     const bool act = t < my_steps;
     const bool acc = t >= 1;  // Julia t > 1 (filter.jl:194)
     if (!act) return;
-    if (meta_c.x != 0.0) {
+    if (meta_c.x != 0.0 || t >= my_data) {
       // NaN column: prediction only (filter.jl:126-140); F, v stale → the loglik
       // re-adds the previous term (filter.jl:195 reads base.F / base.v unchanged).
       double Pf[M][M];
@@ -427,7 +433,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
 #pragma unroll
         for (int j = i; j < M; ++j) Pf[i][j] = sigma2 * W[i][j];
     }
-    const bool upd = !(t == 0 && det == 0.0);  // inv(F) threw at t=1: skip update (filter.jl:151-154)
+    const bool upd = det != 0.0;  // inv(F) threw: return without the update (filter.jl:151-154)
     if (upd) propagate_state<M, LEAD>(p, bf, Pf, beta, Pm);
     last_det = det;
     last_q = upd ? q : __builtin_nan("");
@@ -439,14 +445,18 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   };
   auto record = [&](int t) {
     if constexpr (RECORD) {
-      if (live && t < my_steps) {
-        const size_t o = (size_t)b * (size_t)(T - 1) + t;
+      // the state after step t, into slot t − max(0, my_steps − rec_len) (the last rec_len steps)
+      const int slot = t - max(0, my_steps - rec_len);
+      if (live && t < my_steps && slot >= 0) {
+        const size_t o = (size_t)b * (size_t)rec_len + slot;
 #pragma unroll
         for (int i = 0; i < M; ++i) rec_beta[o * M + i] = beta[i];
+        if (rec_P) {
 #pragma unroll
-        for (int j = 0; j < M; ++j)
+          for (int j = 0; j < M; ++j)
 #pragma unroll
-          for (int i = 0; i < M; ++i) rec_P[o * M * M + j * M + i] = Pm[i][j];
+            for (int i = 0; i < M; ++i) rec_P[o * M * M + j * M + i] = Pm[i][j];
+        }
       }
     }
   };
@@ -583,10 +593,11 @@ static hipError_t launch_fixedz_np(const LaunchArgs& a) {
   const int grid = (a.B + kBlock - 1) / kBlock;
   if (a.rec_beta) {
     hipLaunchKernelGGL((fixedz_loglik_kernel<NP, M, LEAD, true>), dim3(grid), dim3(kBlock), 0, a.stream, a.theta, a.P,
-                       a.B, a.space, a.panel, a.T, a.N, a.mats, a.T_use, a.out, a.flags, a.rec_beta, a.rec_P);
+                       a.B, a.space, a.panel, a.T, a.N, a.mats, a.T_use, a.out, a.flags, a.rec_beta, a.rec_P,
+                       a.horizon, a.rec_len);
   } else {
     hipLaunchKernelGGL((fixedz_loglik_kernel<NP, M, LEAD, false>), dim3(grid), dim3(kBlock), 0, a.stream, a.theta,
-                       a.P, a.B, a.space, a.panel, a.T, a.N, a.mats, a.T_use, a.out, a.flags, nullptr, nullptr);
+                       a.P, a.B, a.space, a.panel, a.T, a.N, a.mats, a.T_use, a.out, a.flags, nullptr, nullptr, 0, 0);
   }
   return hipGetLastError();
 }

@@ -119,7 +119,7 @@ __global__ __launch_bounds__(kTvlBlock) void tvl_loglik_kernel(
     const double* __restrict__ prep, int ldp, int np, int T, int N, int TC, const double* __restrict__ mats,
     int K, const double* __restrict__ gap_d, const int* __restrict__ gap_idx,
     const int* __restrict__ T_use, double* __restrict__ out, unsigned int* __restrict__ flags,
-    double* __restrict__ rec_beta, double* __restrict__ rec_P) {
+    double* __restrict__ rec_beta, double* __restrict__ rec_P, int horizon, int rec_len) {
   constexpr int M = 4;
   constexpr int GPB = kTvlBlock / L;  // filters per block
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -147,7 +147,11 @@ __global__ __launch_bounds__(kTvlBlock) void tvl_loglik_kernel(
   }
   if (tid < K) s_gd[tid] = gap_d[tid];
   __syncthreads();
-  atomicMax(&s_nobs_max, live ? nobs : 0);
+  // loglik mode (horizon = 0) or trajectory mode (horizon ≥ 1: columns 0 .. nobs−1, then
+  // horizon NaN steps — predict, filter.jl:250-282, on forecasting.jl:141's NaN padding)
+  const int my_steps = horizon > 0 ? nobs + horizon : nobs - 1;
+  const int my_data = horizon > 0 ? nobs : nobs - 1;
+  atomicMax(&s_nobs_max, live ? my_steps : 0);
 
   Params<M, 0> p;
   double beta[M], Pm[M][M];
@@ -177,10 +181,9 @@ __global__ __launch_bounds__(kTvlBlock) void tvl_loglik_kernel(
   double sumq = 0.0;
   bool neg = false;
   double last_det = 0.0, last_q = 0.0;  // fresh model: F = 0, F⁻¹ = 0, v = 0 (kalmanbasemodel.jl:65-67)
-  const int my_steps = nobs - 1;
 
   __syncthreads();
-  const int nsteps = max(s_nobs_max - 1, 0);
+  const int nsteps = max(s_nobs_max, 0);
   const int CHY = TC * N;  // yields per chunk
 
   // ---- panel staging: chunk c (columns cTC .. cTC+TC-1) in LDS, chunk c+1 in registers ----
@@ -217,7 +220,7 @@ __global__ __launch_bounds__(kTvlBlock) void tvl_loglik_kernel(
     const int tt = t % TC;
     const bool act = t < my_steps;
     const bool acc = t >= 1;  // Julia t > 1 (filter.jl:194)
-    const bool nan_col = s_nan[tt] != 0.0;
+    const bool nan_col = s_nan[tt] != 0.0 || t >= my_data;
     if (act && nan_col) {
       // filter.jl:13-29: prediction only; F, F⁻¹, v stale → the loglik re-adds the last term
       double bf[M], Pf[M][M];
@@ -341,14 +344,17 @@ __global__ __launch_bounds__(kTvlBlock) void tvl_loglik_kernel(
       }
     }
     if constexpr (RECORD) {
-      if (live && act && j == 0) {
-        const size_t o = (size_t)b * (size_t)(T - 1) + t;
+      const int slot = t - max(0, my_steps - rec_len);  // the last rec_len steps
+      if (live && act && j == 0 && slot >= 0) {
+        const size_t o = (size_t)b * (size_t)rec_len + slot;
 #pragma unroll
         for (int i = 0; i < M; ++i) rec_beta[o * M + i] = beta[i];
+        if (rec_P) {
 #pragma unroll
-        for (int k = 0; k < M; ++k)
+          for (int k = 0; k < M; ++k)
 #pragma unroll
-          for (int i = 0; i < M; ++i) rec_P[o * M * M + k * M + i] = Pm[i][k];
+            for (int i = 0; i < M; ++i) rec_P[o * M * M + k * M + i] = Pm[i][k];
+        }
       }
     }
     if (tt == TC - 1) {  // chunk done: its buffer takes the prefetched chunk, prefetch the one after
@@ -392,11 +398,11 @@ hipError_t launch_tvl_l(const LaunchArgs& a, const TvlGaps& g, int TC) {
   if (a.rec_beta) {
     hipLaunchKernelGGL((tvl_loglik_kernel<L, true>), dim3(grid), dim3(kTvlBlock), shmem, a.stream, a.scratch, a.B,
                        a.raw, a.panel, a.ldp, a.np, a.T, a.N, TC, a.mats, g.K, g.d, g.idx, a.T_use, a.out, a.flags, a.rec_beta,
-                       a.rec_P);
+                       a.rec_P, a.horizon, a.rec_len);
   } else {
     hipLaunchKernelGGL((tvl_loglik_kernel<L, false>), dim3(grid), dim3(kTvlBlock), shmem, a.stream, a.scratch, a.B,
                        a.raw, a.panel, a.ldp, a.np, a.T, a.N, TC, a.mats, g.K, g.d, g.idx, a.T_use, a.out, a.flags, nullptr,
-                       nullptr);
+                       nullptr, 0, 0);
   }
   return hipGetLastError();
 }

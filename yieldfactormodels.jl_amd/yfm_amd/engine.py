@@ -12,7 +12,7 @@ import threading
 import numpy as np
 
 from . import _lib
-from .params import n_params, state_dim
+from .params import gamma_dim, n_params, state_dim
 
 
 class Engine:
@@ -95,6 +95,54 @@ class Engine:
         _lib.check(self.lib.yfm_filter_states(self.ctx, kind, space, _lib.dptr(Th), P, B, _lib.iptr(tu),
                                               _lib.dptr(beta), _lib.dptr(Pm), _lib.dptr(out)))
         return out, beta, Pm
+
+    @staticmethod
+    def _batch(theta, kind):
+        Th = np.asfortranarray(np.atleast_2d(np.asarray(theta, dtype=np.float64).T).T)
+        if Th.shape[0] != n_params(kind):
+            raise ValueError(f"theta has {Th.shape[0]} rows, model kind {kind} needs {n_params(kind)}")
+        return Th
+
+    @staticmethod
+    def _tuse(T_use, B):
+        return None if T_use is None else np.ascontiguousarray(np.broadcast_to(T_use, (B,)), dtype=np.int32)
+
+    def predict(self, kind: int, theta, space: int = 1, T_use=None, horizon: int = 1) -> dict:
+        """predict (filter.jl:250-282) per θ_b on hcat(data[:, :T_b], NaN × (horizon−1)).
+        Returns arrays with a trailing batch axis: preds/factor_loadings_1/2 (N, ncol, B),
+        factors (M, ncol, B), states (L, ncol, B), ncol = T + horizon − 1."""
+        Th = self._batch(theta, kind)
+        P, B = Th.shape
+        M, L, N = state_dim(kind), gamma_dim(kind), self._panel.shape[0]
+        ncol = self.T + horizon - 1
+        preds = np.empty((N, ncol, B), order="F")
+        fl1 = np.empty((N, ncol, B), order="F")
+        fl2 = np.empty((N, ncol, B), order="F")
+        fac = np.empty((M, ncol, B), order="F")
+        st = np.empty((L, ncol, B), order="F")
+        _lib.check(self.lib.yfm_predict(self.ctx, kind, space, _lib.dptr(Th), P, B, _lib.iptr(self._tuse(T_use, B)),
+                                        horizon, _lib.dptr(preds), _lib.dptr(fac), _lib.dptr(st), _lib.dptr(fl1),
+                                        _lib.dptr(fl2)))
+        return dict(preds=preds, factors=fac, states=st, factor_loadings_1=fl1, factor_loadings_2=fl2)
+
+    def forecast(self, kind: int, theta, space: int = 1, T_use=None, horizon: int = 1) -> np.ndarray:
+        """forecasting.jl:236-250 blocks vcat(factors, states, preds)[:, end-h+1:end]: (M+L+N, h, B)."""
+        Th = self._batch(theta, kind)
+        P, B = Th.shape
+        R = state_dim(kind) + gamma_dim(kind) + self._panel.shape[0]
+        out = np.empty((R, horizon, B), order="F")
+        _lib.check(self.lib.yfm_forecast(self.ctx, kind, space, _lib.dptr(Th), P, B, _lib.iptr(self._tuse(T_use, B)),
+                                         horizon, _lib.dptr(out)))
+        return out
+
+    def loss_array(self, kind: int, theta, space: int = 1, T_use=None, K: int = 1) -> np.ndarray:
+        """get_loss_array (filter.jl:211-247) per θ_b: (T−1, B)."""
+        Th = self._batch(theta, kind)
+        P, B = Th.shape
+        out = np.empty((max(self.T - 1, 0), B), order="F")
+        _lib.check(self.lib.yfm_loss_array(self.ctx, kind, space, _lib.dptr(Th), P, B,
+                                           _lib.iptr(self._tuse(T_use, B)), K, _lib.dptr(out)))
+        return out
 
     def last_flags(self):
         a, b = ctypes.c_longlong(0), ctypes.c_longlong(0)

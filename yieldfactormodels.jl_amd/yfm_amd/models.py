@@ -15,6 +15,10 @@ reference                                 here
 ``untransform_params`` parameteroperations.jl:34-60  :func:`untransform_params`
 ``get_loss`` kalman/filter.jl:182-209       :func:`get_loss`
 ``compute_loss`` optimization.jl:10-23      :func:`compute_loss`
+``predict`` kalman/filter.jl:250-282        :func:`predict` (``horizon`` = NaN padding of
+                                            forecasting.jl:141)
+``get_loss_array`` kalman/filter.jl:211-247 :func:`get_loss_array`
+forecast blocks forecasting.jl:236-250      :func:`forecast_batch`
 =======================================  =================================================
 
 plus the batched forms the device boundary exists for: :func:`get_loss_batch` and
@@ -98,7 +102,7 @@ class GNS5Model(AbstractKalmanModel):
 
     def __init__(self, maturities, N: int, M: int = 5, model_string: str = "GNS5", results_location: str = "results/",
                  device: int = 0):
-        self.base = KalmanBaseModel(np.asarray(maturities, dtype=np.float64), N, 5, 1, _p.KIND_GNS, model_string,
+        self.base = KalmanBaseModel(np.asarray(maturities, dtype=np.float64), N, 5, 2, _p.KIND_GNS, model_string,
                                     results_location)
         self.device = device
 
@@ -184,3 +188,45 @@ def filter_states(model: AbstractKalmanModel, data, Theta=None, space: int = 1, 
     if Theta is None:
         Theta = model.base.flat_params
     return eng.filter_states(model.kind, Theta, space=space, T_use=T_use)
+
+
+def predict(model: AbstractKalmanModel, data, horizon: int = 1, Theta=None, space: int = 1, T_use=None):
+    """filter.jl:250-282 — ``predict(model, data)`` for the model's parameters (horizon = 1), or
+    ``predict(model, hcat(data[:, 1:T_b], NaN × (horizon − 1)))`` as the forecasting driver calls it
+    (forecasting.jl:141, :181-183).  With ``Theta`` (P×B) the call is batched and every array gets a
+    trailing batch axis; otherwise returns the reference's named tuple of N×n / M×n / L×n arrays,
+    n = T + horizon − 1."""
+    eng = _engine(model, data)
+    single = Theta is None
+    if single:
+        Theta = model.base.flat_params
+    out = eng.predict(model.kind, Theta, space=space, T_use=T_use, horizon=horizon)
+    if single:
+        out = {k: v[:, :, 0] for k, v in out.items()}
+        if np.isnan(out["factors"]).all():
+            raise SingularException("initialize_filter: singular I - Φ or I - Φ⊗Φ")
+    return out
+
+
+def get_loss_array(model: AbstractKalmanModel, data, K: int = 1, Theta=None, space: int = 1, T_use=None):
+    """filter.jl:211-247: the per-step −‖y_t − ŷ_t‖²/N/K (length T−1), or the scalar −Inf where the
+    reference returns it.  With ``Theta`` (P×B): a (T−1)×B array, −Inf rows for −Inf candidates."""
+    eng = _engine(model, data)
+    single = Theta is None
+    out = eng.loss_array(model.kind, model.base.flat_params if single else Theta, space=space, T_use=T_use, K=K)
+    if single:
+        row = out[:, 0]
+        if np.isnan(row).all() and row.size:
+            raise SingularException("initialize_filter: singular I - Φ or I - Φ⊗Φ")
+        if row.size and np.isneginf(row).all():
+            return -np.inf
+        return row
+    return out
+
+
+def forecast_batch(model: AbstractKalmanModel, data, Theta, T_use, horizon: int, space: int = 1) -> np.ndarray:
+    """The rolling-window driver's per-task record (forecasting.jl:236-250): for window b,
+    ``vcat(factors, states, preds)[:, end-h+1:end]`` of predict on hcat(data[:, 1:T_use[b]], NaN × (h−1)).
+    Returns (M + L + N, h, B)."""
+    eng = _engine(model, data)
+    return eng.forecast(model.kind, Theta, space=space, T_use=T_use, horizon=horizon)

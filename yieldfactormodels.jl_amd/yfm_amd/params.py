@@ -55,6 +55,11 @@ def state_dim(kind: int) -> int:
     return {KIND_DNS: 3, KIND_TVL: 4, KIND_GNS: 5}[kind]
 
 
+def gamma_dim(kind: int) -> int:
+    """L = length of base.gamma (kalmanbasemodel.jl:58), reported by predict as `states`."""
+    return {KIND_DNS: 1, KIND_TVL: 1, KIND_GNS: 2}[kind]
+
+
 def param_layout(kind: int) -> ParamLayout:
     M = state_dim(kind)
     n_lead = {KIND_DNS: 1, KIND_TVL: 0, KIND_GNS: 2}[kind]
