@@ -137,6 +137,22 @@ int yfm_forecast(yfm_ctx* ctx, int model_kind, int param_space, const double* th
 int yfm_loss_array(yfm_ctx* ctx, int model_kind, int param_space, const double* theta, int P, int B,
                    const int* T_use, int K, double* mse_out);
 
+/* Batched estimation — replaces R calls of estimate_steps! (optimization.jl:137-312) for
+ * a Kalman model with every parameter in group "1" (kalmanbasemodel.jl:150-159), i.e.
+ * block-coordinate Nelder–Mead (Optim.NelderMead(), opt1: `iterations`, `g_tol`;
+ * optimization.jl:442-451, :479) with the outer loop max_group_iters / |ΔLL| < tol.
+ * Chain r starts from theta0[:, r] (param_space as above; the reference receives
+ * constrained all_params and untransforms them) on the window Y[:, 1:T_use[r]] (or all
+ * T columns when T_use is NULL).  The R chains' objective evaluations are batched into
+ * one device launch per round.  Outputs: theta_c_out P×R = transform_params(best_p)
+ * (the reference's returned params), p_out P×R unconstrained optimum (or NULL), ll_out R
+ * (the reference's returned ll), status_out R (or NULL): 0 ok, 1 the reference would
+ * throw (NaN outputs), 2 aborted after the first group iteration (parameters kept);
+ * n_evals_out (or NULL): objective evaluations performed.  Synchronous. */
+int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const double* theta0, int P, int R,
+                 const int* T_use, int iterations, double g_tol, int max_group_iters, double tol,
+                 double* theta_c_out, double* p_out, double* ll_out, int* status_out, long long* n_evals_out);
+
 /* Counters of the last completed batch on this ctx: candidates where the
  * reference would have thrown (NaN outputs) and candidates returning -Inf.
  * For yfm_loglik_batch_device, synchronise the stream first. */

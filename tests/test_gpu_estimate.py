@@ -1,0 +1,123 @@
+"""GPU parity of the batched estimation driver: yfm_estimate (R
+estimate_steps! chains, Nelder–Mead per Optim.jl's published algorithm, every round of all
+chains evaluated in one device launch) vs oracle/optim_nm.py (a sequential restatement of
+estimate_steps! + Optim.NelderMead).
+
+* Bit for bit when both drive the SAME objective values: the oracle's objective is the
+  device loglik of one θ at a time, so any difference is a difference in the optimiser
+  state machine (branching, ordering, simplex arithmetic, stopping rules, exceptions).
+* Against the fully independent CPU path (oracle chain over the C restatement of the
+  reference filter): the final loglik within 1e-9 relative.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from oracle import optim_nm as NM
+from yfm_amd import KIND_DNS
+from yfm_amd import synthetic as S
+from yfm_amd.params import param_layout, transform_params, untransform_params
+
+pytestmark = pytest.mark.gpu
+
+
+def device_objective(engine, kind, window):
+    def f(theta):
+        ll = engine.loglik(kind, np.asarray(theta)[:, None], space=0, T_use=None if window is None else [window])[0]
+        if math.isnan(ll):
+            raise NM.InitThrow()
+        return -ll
+    return f
+
+
+@pytest.fixture(scope="module")
+def panel():
+    return S.simulate_panel(KIND_DNS, 600)[:, :80].copy(order="F"), S.maturities_30()
+
+
+def test_estimate_bitwise_vs_oracle_chain(engine, panel):
+    """Three windows, unconstrained starts, 150 Nelder–Mead iterations × up to 2 group iterations."""
+    Y, mats = panel
+    engine.set_panel(Y, mats)
+    starts = S.theta_batch(KIND_DNS, 3, seed=61, bad_frac=0.0, scale=0.05)
+    win = np.array([80, 60, 45], dtype=np.int32)
+    got = engine.estimate(KIND_DNS, starts, space=0, T_use=win, iterations=150, max_group_iters=2)
+    for r in range(3):
+        ref = NM.estimate_steps(device_objective(engine, KIND_DNS, int(win[r])), starts[:, r],
+                                transform=lambda x: transform_params(KIND_DNS, x), untransform=lambda x: x,
+                                max_group_iters=2, iterations=150)
+        assert got["status"][r] == ref.status == 0
+        np.testing.assert_array_equal(got["p"][:, r], ref.p)
+        assert got["ll"][r] == ref.ll
+        np.testing.assert_allclose(got["theta_c"][:, r], ref.theta_c, rtol=1e-15)
+        assert np.isfinite(ref.ll) and ref.ll > engine.loglik(KIND_DNS, starts[:, r], space=0, T_use=[win[r]])[0]
+
+
+def test_estimate_rescaled_start_and_throw(engine, panel):
+    """A start whose loglik is −Inf goes through the ×0.95 rescaling (optimization.jl:173-184); a
+    constrained start with Φ = I makes compute_loss throw → status 1, NaN outputs."""
+    Y, mats = panel
+    engine.set_panel(Y, mats)
+    cand = S.theta_batch(KIND_DNS, 4096, seed=63, bad_frac=0.05)
+    ll = engine.loglik(KIND_DNS, cand, space=0)
+    bad = cand[:, np.flatnonzero(np.isneginf(ll))[:1]]
+    assert bad.shape[1] == 1
+    got = engine.estimate(KIND_DNS, bad, space=0, iterations=60, max_group_iters=1)
+    ref = NM.estimate_steps(device_objective(engine, KIND_DNS, None), bad[:, 0],
+                            transform=lambda x: transform_params(KIND_DNS, x), untransform=lambda x: x,
+                            max_group_iters=1, iterations=60)
+    assert got["status"][0] == ref.status
+    np.testing.assert_array_equal(got["p"][:, 0], ref.p)
+    assert got["ll"][0] == ref.ll or (math.isinf(ref.ll) and got["ll"][0] == ref.ll)
+
+    th = S.theta0_constrained(KIND_DNS)
+    lay = param_layout(KIND_DNS)
+    th[lay.phi_offset:lay.phi_offset + 9] = np.eye(3).reshape(-1)
+    got = engine.estimate(KIND_DNS, th, space=1, iterations=10, max_group_iters=1)
+    assert got["status"][0] == 1 and np.isnan(got["ll"][0]) and np.isnan(got["theta_c"]).all()
+
+
+def test_estimate_vs_cpu_reference_path(engine, panel):
+    """The whole chain on the independent CPU path (the C restatement of the reference filter,
+    oracle/yfm_oracle.c, one θ per call) reaches the same optimum."""
+    Y, mats = panel
+    Y = Y[:, :50].copy(order="F")
+    engine.set_panel(Y, mats)
+    lib = ctypes.CDLL(str(ROOT / "oracle" / "libyfm_oracle.so"))
+    D = ctypes.POINTER(ctypes.c_double)
+
+    def f(theta):
+        th = np.ascontiguousarray(theta, dtype=np.float64)
+        out = np.empty(1)
+        lib.yfm_oracle_loglik(KIND_DNS, 0, Y.ctypes.data_as(D), 30, 50, mats.ctypes.data_as(D), th.ctypes.data_as(D),
+                              20, 1, None, out.ctypes.data_as(D), 1)
+        if math.isnan(out[0]):
+            raise NM.InitThrow()
+        return -out[0]
+
+    th0 = S.theta0_constrained(KIND_DNS)
+    ref = NM.estimate_steps(f, th0, transform=lambda x: transform_params(KIND_DNS, x),
+                            untransform=lambda x: untransform_params(KIND_DNS, x), max_group_iters=1, iterations=80)
+    got = engine.estimate(KIND_DNS, th0, space=1, iterations=80, max_group_iters=1)
+    assert got["status"][0] == ref.status == 0
+    assert abs(got["ll"][0] - ref.ll) <= 1e-9 * abs(ref.ll)
+    np.testing.assert_allclose(got["theta_c"][:, 0], ref.theta_c, rtol=1e-7, atol=1e-9)
+
+
+def test_estimate_steps_model_api(engine, panel):
+    """estimate_steps!(model, data, all_params, param_groups) returns (init_p, ll, best_p, ir)."""
+    from yfm_amd import create_model, estimate_steps_, get_loss, set_params_
+    Y, mats = panel
+    model, _ = create_model("1C", mats, 30)
+    th0 = S.theta0_constrained(KIND_DNS)
+    init_p, ll, best_p, ir = estimate_steps_(model, Y, th0[:, None], ["1"] * 20, max_group_iters=1)
+    np.testing.assert_array_equal(init_p, th0)
+    set_params_(model, best_p)
+    assert abs(get_loss(model, Y) - ll) <= 1e-12 * abs(ll)
+    set_params_(model, th0)
+    assert ll > get_loss(model, Y)

@@ -282,6 +282,10 @@ int validate_tuse(const int* T_use, int B, int T) {
 
 }  // namespace
 
+namespace yfm {
+int api_error(int code, const char* msg) { return set_error(code, "%s", msg); }
+}  // namespace yfm
+
 extern "C" {
 
 int yfm_abi_version(void) { return YFM_ABI_VERSION; }

@@ -1,0 +1,395 @@
+// yfm_estimate.hip — batched estimation driver: R independent estimate_steps! chains
+// (one per estimation window / start) whose objective evaluations are gathered, round by
+// round, into ONE batched log-likelihood launch on the device (yfm_loglik_batch).
+//
+// Restates, per chain (reference paths relative to the reference root):
+//   estimate_steps!   src/optimization.jl:137-312 for a Kalman model, all parameters in
+//                     group "1" (kalmanbasemodel.jl:150-159): untransform + sanitize
+//                     (:157-162, :422-432), ×0.95 rescaling of a non-finite start
+//                     (:173-184), outer loop max_group_iters / |ΔLL| < tol (:218-281),
+//                     rethrow on iteration 1 / abort later (:249-257), transform (:301).
+//   Optim.NelderMead  with opt1 (iterations = 500, g_tol = 1e-6; optimization.jl:442-451,
+//                     :479).  Optim.jl 1.13 (Project.toml:42) is not vendored in the
+//                     reference; its published algorithm (adaptive parameters, affine
+//                     simplexer, reflection / expansion / contractions / shrink, nm_x
+//                     stopping rule, centroid-vs-best minimizer) is restated here and in
+//                     oracle/optim_nm.py, against which this file is tested bit for bit.
+//
+// MI355X mapping: the chains are independent, so every round packs the points all
+// chains need into one batch and evaluates it with one kernel launch.  A Nelder–Mead
+// iteration needs the reflection and then, depending on it, one of expansion / outside
+// contraction / inside contraction: all four are functions of (centroid, worst vertex),
+// so one round evaluates them speculatively and the chain then takes exactly the
+// reference's branch (unused values are discarded, including their failures).  A shrink
+// costs one extra round.  The arithmetic of the simplex updates follows Optim's
+// operation order with FP contraction off, so the chain is bitwise reproducible.
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+#include "../../include/yfm.h"
+#include "yfm_internal.hpp"
+
+namespace {
+
+enum Code { ID = 0, POS = 1, R11 = 2 };
+
+// transform vectors: kalmanbasemodel.jl:74-120 (+ dns.jl:15-22 one leading γ; GNS5 two)
+std::vector<int> transform_codes(int kind) {
+  const int M = yfm_state_dim(kind);
+  const int lead = kind == YFM_MODEL_DNS ? 1 : kind == YFM_MODEL_GNS5 ? 2 : 0;
+  std::vector<int> c(lead, ID);
+  c.push_back(POS);  // σ²
+  for (int i = 0; i < M; ++i)
+    for (int j = 0; j <= i; ++j) c.push_back(j == i ? POS : ID);  // U by column, diag exp
+  for (int i = 0; i < M; ++i) c.push_back(ID);                   // δ
+  for (int i = 0; i < M; ++i)
+    for (int j = 0; j < M; ++j) c.push_back(i == j ? R11 : ID);  // Φ row-major
+  return c;
+}
+
+// transformations.jl:2-26
+double to_constrained(int code, double x) {
+  if (code == POS) return std::exp(x);
+  if (code == R11) {
+    const double y = std::exp(x);
+    return 2.0 * y / (1.0 + y) - 1.0;
+  }
+  return x;
+}
+double to_unconstrained(int code, double x) {
+  if (code == POS) return std::log(x);
+  if (code == R11) return std::log1p(x) - std::log1p(-x);
+  return x;
+}
+
+enum Phase { VALIDATE, NM_INIT, NM_ITER, NM_SHRINK, NM_FINAL, DONE };
+
+struct Chain {
+  int n = 0;                // parameters (simplex dimension)
+  Phase phase = VALIDATE;
+  int window = 0;           // T_use of this chain
+  std::vector<double> p;    // current unconstrained parameters
+  int rescales = 0;
+  double prev_ll = -INFINITY;
+  int outer = 0;            // group iteration (1-based once the first Nelder–Mead starts)
+  int status = YFM_OK;      // 0 ok, 1 the reference throws, 2 aborted after iteration 1
+  // Nelder–Mead state (Optim's NelderMeadState)
+  std::vector<double> S;    // (n+1) × n vertices, row v = vertex v
+  std::vector<double> fs;   // n+1 vertex values
+  std::vector<int> order;   // stable sortperm of fs
+  int it = 0;
+  bool converged = false;
+  std::vector<double> xc, xl, trial;  // centroid, best vertex, requested points
+  int n_req = 0;
+  size_t req_off = 0;
+};
+
+void sortperm(Chain& c) {
+  std::iota(c.order.begin(), c.order.end(), 0);
+  std::stable_sort(c.order.begin(), c.order.end(), [&](int a, int b) {
+    const double fa = c.fs[a], fb = c.fs[b];
+    if (std::isnan(fa) || std::isnan(fb)) return !std::isnan(fa) && std::isnan(fb);
+    return fa < fb;
+  });
+}
+
+// centroid of all vertices but h: storage-order sum × (1/n)   (Optim centroid!)
+void centroid(const Chain& c, int h, double* out) {
+  const int n = c.n;
+  for (int k = 0; k < n; ++k) out[k] = 0.0;
+  for (int v = 0; v <= n; ++v) {
+    if (v == h) continue;
+    const double* x = &c.S[(size_t)v * n];
+    for (int k = 0; k < n; ++k) out[k] = out[k] + x[k];
+  }
+  const double r = 1.0 / n;
+  for (int k = 0; k < n; ++k) out[k] = out[k] * r;
+}
+
+// sqrt(var(f) · n/(n+1)): population standard deviation of the vertex values
+double nm_x(const Chain& c) {
+  const int m = c.n + 1;
+  double s = 0.0;
+  for (int v = 0; v < m; ++v) s = s + c.fs[v];
+  const double mu = s / m;
+  double q = 0.0;
+  for (int v = 0; v < m; ++v) {
+    const double d = c.fs[v] - mu;
+    q = q + d * d;
+  }
+  return std::sqrt(q / (m - 1) * ((double)(m - 1) / m));
+}
+
+struct Params {
+  double al, be, ga, de;
+};
+
+Params nm_parameters(int n) {  // Optim.AdaptiveParameters: (α, β + 2/n, γ − 1/2n, δ − 1/n)
+  return {1.0, 1.0 + 2.0 / n, 0.75 - 1.0 / (2.0 * n), 1.0 - 1.0 / n};
+}
+
+// Queue the points chain c needs this round; advances phases that need no evaluation.
+void prepare(Chain& c, int iterations, std::vector<double>& batch, std::vector<int>& tuse) {
+  const int n = c.n, m = n + 1;
+  c.n_req = 0;
+  if (c.phase == NM_ITER && (c.converged || c.it >= iterations)) c.phase = NM_FINAL;
+  c.trial.clear();
+  switch (c.phase) {
+    case VALIDATE:
+      c.trial = c.p;
+      break;
+    case NM_INIT: {  // AffineSimplexer(a = 0.025, b = 0.5)
+      c.S.assign((size_t)m * n, 0.0);
+      for (int v = 0; v < m; ++v) std::copy(c.p.begin(), c.p.end(), c.S.begin() + (size_t)v * n);
+      for (int j = 0; j < n; ++j) {
+        double& x = c.S[(size_t)(j + 1) * n + j];
+        x = (1.0 + 0.5) * x + 0.025;
+      }
+      c.fs.assign(m, 0.0);
+      c.order.assign(m, 0);
+      c.it = 0;
+      c.converged = false;
+      c.trial = c.S;
+      break;
+    }
+    case NM_ITER: {
+      const Params q = nm_parameters(n);
+      c.xc.assign(n, 0.0);
+      centroid(c, c.order[m - 1], c.xc.data());
+      const double* xh = &c.S[(size_t)c.order[m - 1] * n];
+      c.trial.assign((size_t)4 * n, 0.0);
+      double* xr = &c.trial[0];
+      for (int k = 0; k < n; ++k) xr[k] = c.xc[k] + q.al * (c.xc[k] - xh[k]);
+      for (int k = 0; k < n; ++k) {
+        const double d = xr[k] - c.xc[k];
+        c.trial[n + k] = c.xc[k] + q.be * d;          // expansion
+        c.trial[2 * n + k] = c.xc[k] + q.ga * d;      // outside contraction
+        c.trial[3 * n + k] = c.xc[k] - q.ga * d;      // inside contraction
+      }
+      break;
+    }
+    case NM_SHRINK: {
+      const Params q = nm_parameters(n);
+      c.trial.assign((size_t)n * n, 0.0);
+      for (int i = 1; i < m; ++i) {
+        double* x = &c.S[(size_t)c.order[i] * n];
+        for (int k = 0; k < n; ++k) x[k] = c.xl[k] + q.de * (x[k] - c.xl[k]);
+        std::copy(x, x + n, c.trial.begin() + (size_t)(i - 1) * n);
+      }
+      break;
+    }
+    case NM_FINAL: {  // after_while!: centroid of all but the worst, after a final sortperm
+      sortperm(c);
+      c.xc.assign(n, 0.0);
+      centroid(c, c.order[m - 1], c.xc.data());
+      c.trial = c.xc;
+      break;
+    }
+    case DONE:
+      return;
+  }
+  c.n_req = (int)(c.trial.size() / n);
+  c.req_off = batch.size() / n;
+  batch.insert(batch.end(), c.trial.begin(), c.trial.end());
+  tuse.insert(tuse.end(), c.n_req, c.window);
+}
+
+// objective values −loglik of this chain's requests; NaN ⇔ compute_loss threw
+void fail(Chain& c) {
+  // the optimizer threw: rethrown on the first group iteration (the estimation fails),
+  // later the chain keeps its parameters and stops (optimization.jl:249-257)
+  c.status = c.outer <= 1 ? 1 : 2;
+  c.phase = DONE;
+}
+
+void consume(Chain& c, const double* f, int max_group_iters, double tol, double g_tol) {
+  const int n = c.n, m = n + 1;
+  switch (c.phase) {
+    case VALIDATE: {
+      if (std::isnan(f[0])) {
+        c.status = 1;
+        c.phase = DONE;
+        return;
+      }
+      const double ll = -f[0];
+      if (!std::isfinite(ll) && c.rescales < 10) {
+        for (double& x : c.p) x = x * 0.95;
+        ++c.rescales;
+        return;
+      }
+      c.outer = 1;
+      c.phase = NM_INIT;
+      return;
+    }
+    case NM_INIT:
+      for (int v = 0; v < m; ++v) {
+        if (std::isnan(f[v])) return fail(c);
+        c.fs[v] = f[v];
+      }
+      sortperm(c);
+      c.phase = NM_ITER;
+      return;
+    case NM_ITER: {
+      ++c.it;
+      const int il = c.order[0], ish = c.order[n - 1], ih = c.order[m - 1];
+      const double fl = c.fs[il], fsh = c.fs[ish], fh = c.fs[ih];
+      c.xl.assign(c.S.begin() + (size_t)il * n, c.S.begin() + (size_t)(il + 1) * n);
+      const double fr = f[0];
+      if (std::isnan(fr)) return fail(c);
+      double* xh = &c.S[(size_t)ih * n];
+      const double* xr = &c.trial[0];
+      bool shrink = false;
+      if (fr < fl) {
+        const double fe = f[1];
+        if (std::isnan(fe)) return fail(c);
+        if (fe < fr) {
+          std::copy(&c.trial[n], &c.trial[2 * n], xh);
+          c.fs[ih] = fe;
+        } else {
+          std::copy(xr, xr + n, xh);
+          c.fs[ih] = fr;
+        }
+        for (int i = m - 1; i >= 1; --i) c.order[i] = c.order[i - 1];  // the new vertex is the lowest
+        c.order[0] = ih;
+      } else if (fr < fsh) {
+        std::copy(xr, xr + n, xh);
+        c.fs[ih] = fr;
+        sortperm(c);
+      } else if (fr < fh) {
+        const double fo = f[2];
+        if (std::isnan(fo)) return fail(c);
+        if (fo < fr) {
+          std::copy(&c.trial[2 * n], &c.trial[3 * n], xh);
+          c.fs[ih] = fo;
+          sortperm(c);
+        } else {
+          shrink = true;
+        }
+      } else {
+        const double fi = f[3];
+        if (std::isnan(fi)) return fail(c);
+        if (fi < fh) {
+          std::copy(&c.trial[3 * n], &c.trial[4 * n], xh);
+          c.fs[ih] = fi;
+          sortperm(c);
+        } else {
+          shrink = true;
+        }
+      }
+      if (shrink) {
+        c.phase = NM_SHRINK;
+        return;
+      }
+      c.converged = nm_x(c) <= g_tol;
+      return;
+    }
+    case NM_SHRINK:
+      for (int i = 1; i < m; ++i) {
+        if (std::isnan(f[i - 1])) return fail(c);
+        c.fs[c.order[i]] = f[i - 1];
+      }
+      sortperm(c);
+      c.converged = nm_x(c) <= g_tol;
+      c.phase = NM_ITER;
+      return;
+    case NM_FINAL: {
+      const double fcm = f[0];
+      if (std::isnan(fcm)) return fail(c);
+      int imin = 0;
+      for (int v = 1; v < m; ++v)
+        if (c.fs[v] < c.fs[imin]) imin = v;  // findmin: first minimum
+      double fmin = c.fs[imin];
+      const double* xmin = &c.S[(size_t)imin * n];
+      if (fcm < fmin) {
+        xmin = c.xc.data();
+        fmin = fcm;
+      }
+      c.p.assign(xmin, xmin + n);
+      // ll = −loss_wrapper(p) (:269): the objective at the minimizer, already evaluated
+      const double ll = -fmin;
+      const double d = ll - c.prev_ll;
+      if (std::fabs(d) < tol) {
+        c.prev_ll = ll;
+        c.phase = DONE;
+        return;
+      }
+      c.prev_ll = ll;
+      if (c.outer >= max_group_iters) {
+        c.phase = DONE;
+        return;
+      }
+      ++c.outer;
+      c.phase = NM_INIT;
+      return;
+    }
+    case DONE:
+      return;
+  }
+}
+
+}  // namespace
+
+extern "C" int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const double* theta0, int P, int R,
+                            const int* T_use, int iterations, double g_tol, int max_group_iters, double tol,
+                            double* theta_c_out, double* p_out, double* ll_out, int* status_out,
+                            long long* n_evals_out) {
+  if (!ctx) return yfm::api_error(YFM_EINVAL, "null context");
+  if (yfm_param_count(model_kind) < 0) return yfm::api_error(YFM_EINVAL, "unknown model_kind");
+  if (P != yfm_param_count(model_kind)) return yfm::api_error(YFM_EINVAL, "P does not match model_kind");
+  if (param_space != YFM_THETA_UNCONSTRAINED && param_space != YFM_THETA_CONSTRAINED)
+    return yfm::api_error(YFM_EINVAL, "unknown param_space");
+  if (R < 0 || iterations < 0 || max_group_iters < 1)
+    return yfm::api_error(YFM_EINVAL, "R, iterations must be >= 0 and max_group_iters >= 1");
+  if (R == 0) return YFM_OK;
+  if (!theta0 || !theta_c_out || !ll_out) return yfm::api_error(YFM_EINVAL, "null pointer argument");
+  const std::vector<int> codes = transform_codes(model_kind);
+  std::vector<Chain> chains(R);
+  for (int r = 0; r < R; ++r) {
+    Chain& c = chains[r];
+    c.n = P;
+    c.window = T_use ? T_use[r] : 0;
+    c.p.resize(P);
+    for (int i = 0; i < P; ++i) {
+      double x = theta0[(size_t)r * P + i];
+      if (param_space == YFM_THETA_CONSTRAINED) x = to_unconstrained(codes[i], x);
+      c.p[i] = std::isfinite(x) ? x : 0.0;  // _sanitize_parameters (optimization.jl:422-432)
+    }
+  }
+  std::vector<double> batch, out;
+  std::vector<int> tuse;
+  long long evals = 0;
+  for (;;) {
+    batch.clear();
+    tuse.clear();
+    for (Chain& c : chains) prepare(c, iterations, batch, tuse);
+    const int B = (int)(batch.size() / P);
+    if (B == 0) break;
+    out.resize(B);
+    const int rc = yfm_loglik_batch(ctx, model_kind, YFM_THETA_UNCONSTRAINED, batch.data(), P, B,
+                                    T_use ? tuse.data() : nullptr, out.data());
+    if (rc != YFM_OK) return rc;
+    evals += B;
+    for (double& v : out) v = -v;  // compute_loss = −loglik (optimization.jl:22)
+    for (Chain& c : chains)
+      if (c.n_req > 0) consume(c, out.data() + c.req_off, max_group_iters, tol, g_tol);
+  }
+  for (int r = 0; r < R; ++r) {
+    const Chain& c = chains[r];
+    const bool ok = c.status != 1;
+    for (int i = 0; i < P; ++i) {
+      theta_c_out[(size_t)r * P + i] = ok ? to_constrained(codes[i], c.p[i]) : NAN;
+      if (p_out) p_out[(size_t)r * P + i] = c.p[i];
+    }
+    ll_out[r] = ok ? c.prev_ll : NAN;
+    if (status_out) status_out[r] = c.status;
+  }
+  if (n_evals_out) *n_evals_out = evals;
+  return YFM_OK;
+}

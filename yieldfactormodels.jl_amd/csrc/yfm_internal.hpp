@@ -61,6 +61,8 @@ hipError_t launch_init_bad(const double* ll, int B, unsigned char* bad, hipStrea
 hipError_t launch_predict_emit(const PredictArgs& a);
 hipError_t launch_forecast_emit(const PredictArgs& a);
 hipError_t launch_loss_array(const PredictArgs& a, const double* Y, int T1, int passes, unsigned int* flags);
+// record `msg` as yfm_last_error() for this thread and return `code` (host helpers above the C ABI)
+int api_error(int code, const char* msg);
 hipError_t launch_prep_panel(const double* Y, int N, int T, int np, int ldp, double* out, hipStream_t s);
 
 }  // namespace yfm

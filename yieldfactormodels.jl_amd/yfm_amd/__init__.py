@@ -7,7 +7,7 @@ model / objective API (see :mod:`yfm_amd.models`).
 from .params import (KIND_DNS, KIND_GNS, KIND_TVL, SPACE_CONSTRAINED, SPACE_UNCONSTRAINED, gamma_dim, n_params,
                      param_layout, state_dim)
 from .models import (DNSModel, GNS5Model, SingularException, TVLambdaDNSModel, compute_loss, compute_loss_batch,
-                     create_model, filter_states, forecast_batch, get_loss, get_loss_array, get_loss_batch,
+                     create_model, estimate_batch, estimate_steps_, filter_states, forecast_batch, get_loss, get_loss_array, get_loss_batch,
                      get_params, predict, set_params_, transform_params, untransform_params)
 from .engine import Engine, get_engine
 
@@ -15,6 +15,6 @@ __all__ = [
     "KIND_DNS", "KIND_TVL", "KIND_GNS", "SPACE_CONSTRAINED", "SPACE_UNCONSTRAINED", "n_params", "param_layout",
     "state_dim", "DNSModel", "TVLambdaDNSModel", "GNS5Model", "SingularException", "create_model", "get_params",
     "set_params_", "transform_params", "untransform_params", "get_loss", "compute_loss", "get_loss_batch",
-    "compute_loss_batch", "filter_states", "predict", "get_loss_array", "forecast_batch", "gamma_dim", "Engine",
+    "compute_loss_batch", "filter_states", "estimate_steps_", "estimate_batch", "predict", "get_loss_array", "forecast_batch", "gamma_dim", "Engine",
     "get_engine",
 ]

@@ -38,6 +38,8 @@ SIGNATURES = {
                                    _D, _D, _D, _D, _D]),
     "yfm_forecast": (ctypes.c_int, [_V, ctypes.c_int, ctypes.c_int, _D, ctypes.c_int, ctypes.c_int, _I, ctypes.c_int,
                                     _D]),
+    "yfm_estimate": (ctypes.c_int, [_V, ctypes.c_int, ctypes.c_int, _D, ctypes.c_int, ctypes.c_int, _I, ctypes.c_int,
+                                    ctypes.c_double, ctypes.c_int, ctypes.c_double, _D, _D, _D, _I, _LL]),
     "yfm_loss_array": (ctypes.c_int, [_V, ctypes.c_int, ctypes.c_int, _D, ctypes.c_int, ctypes.c_int, _I, ctypes.c_int,
                                       _D]),
 }

@@ -144,6 +144,22 @@ class Engine:
                                            _lib.iptr(self._tuse(T_use, B)), K, _lib.dptr(out)))
         return out
 
+    def estimate(self, kind: int, theta0, space: int = 1, T_use=None, iterations: int = 500, g_tol: float = 1e-6,
+                 max_group_iters: int = 10, tol: float = 1e-8) -> dict:
+        """Batched estimate_steps! (optimization.jl:137-312): one Nelder–Mead chain per column of Θ₀ (P×R),
+        on window T_use[r].  Returns theta_c (P×R), p (P×R unconstrained), ll (R), status (R), n_evals."""
+        Th = self._batch(theta0, kind)
+        P, R = Th.shape
+        th_c = np.empty((P, R), order="F")
+        p = np.empty((P, R), order="F")
+        ll = np.empty(R)
+        st = np.empty(R, dtype=np.int32)
+        ne = ctypes.c_longlong(0)
+        _lib.check(self.lib.yfm_estimate(self.ctx, kind, space, _lib.dptr(Th), P, R, _lib.iptr(self._tuse(T_use, R)),
+                                         iterations, g_tol, max_group_iters, tol, _lib.dptr(th_c), _lib.dptr(p),
+                                         _lib.dptr(ll), _lib.iptr(st), ctypes.byref(ne)))
+        return dict(theta_c=th_c, p=p, ll=ll, status=st, n_evals=ne.value)
+
     def last_flags(self):
         a, b = ctypes.c_longlong(0), ctypes.c_longlong(0)
         _lib.check(self.lib.yfm_last_batch_flags(self.ctx, ctypes.byref(a), ctypes.byref(b)))

@@ -19,6 +19,8 @@ reference                                 here
                                             forecasting.jl:141)
 ``get_loss_array`` kalman/filter.jl:211-247 :func:`get_loss_array`
 forecast blocks forecasting.jl:236-250      :func:`forecast_batch`
+``estimate_steps!`` optimization.jl:137-312 :func:`estimate_steps_` (+ batched
+                                            :func:`estimate_batch`)
 =======================================  =================================================
 
 plus the batched forms the device boundary exists for: :func:`get_loss_batch` and
@@ -230,3 +232,33 @@ def forecast_batch(model: AbstractKalmanModel, data, Theta, T_use, horizon: int,
     Returns (M + L + N, h, B)."""
     eng = _engine(model, data)
     return eng.forecast(model.kind, Theta, space=space, T_use=T_use, horizon=horizon)
+
+
+class EstimationError(RuntimeError):
+    """estimate_steps! rethrows from the first group iteration (optimization.jl:249-253)."""
+
+
+def estimate_steps_(model: AbstractKalmanModel, data, all_params, param_groups=None, max_group_iters: int = 10,
+                    tol: float = 1e-8, printing: bool = False):
+    """estimate_steps! (optimization.jl:137-312) for a Kalman model: all_params (P×n, constrained; Kalman
+    models use column 1 only, :153) → (init_p, ll, best_p, ir) with best_p constrained, like the reference.
+    Parameter groups other than all-"1" are not supported (the Kalman default, kalmanbasemodel.jl:150-159)."""
+    A = np.asarray(all_params, dtype=np.float64)
+    start = A[:, 0] if A.ndim == 2 else A
+    if param_groups is not None and any(g != "1" for g in param_groups):
+        raise NotImplementedError("Kalman models estimate every parameter in group \"1\"")
+    r = estimate_batch(model, data, start[:, None], max_group_iters=max_group_iters, tol=tol)
+    if r["status"][0] == 1:
+        raise EstimationError("compute_loss threw on the first group iteration (singular initialize_filter)")
+    if printing:
+        print(f"✓ Best overall LL = {r['ll'][0]} from start 1")
+    return start.copy(), float(r["ll"][0]), r["theta_c"][:, 0].copy(), 0
+
+
+def estimate_batch(model: AbstractKalmanModel, data, Theta0, T_use=None, space: int = 1, iterations: int = 500,
+                   g_tol: float = 1e-6, max_group_iters: int = 10, tol: float = 1e-8) -> dict:
+    """R independent estimate_steps! chains (windows × starts) whose objective evaluations share one device
+    launch per round (libyfm_hip.so: yfm_estimate).  Θ₀: P×R starts (constrained by default, as all_params)."""
+    eng = _engine(model, data)
+    return eng.estimate(model.kind, Theta0, space=space, T_use=T_use, iterations=iterations, g_tol=g_tol,
+                        max_group_iters=max_group_iters, tol=tol)
