@@ -75,10 +75,17 @@ def test_estimate_rescaled_start_and_throw(engine, panel):
     np.testing.assert_array_equal(got["p"][:, 0], ref.p)
     assert got["ll"][0] == ref.ll or (math.isinf(ref.ll) and got["ll"][0] == ref.ll)
 
+    # constrained Φ = I untransforms to +Inf on the diagonal, which _sanitize_parameters zeroes
+    # (optimization.jl:157-162, :422-432): no throw
     th = S.theta0_constrained(KIND_DNS)
     lay = param_layout(KIND_DNS)
     th[lay.phi_offset:lay.phi_offset + 9] = np.eye(3).reshape(-1)
     got = engine.estimate(KIND_DNS, th, space=1, iterations=10, max_group_iters=1)
+    assert got["status"][0] == 0 and got["p"][lay.phi_offset, 0] != 0.0
+    # an unconstrained start with Φ diagonal 40 decodes to exactly Φ = I: initialize_filter throws
+    tu = S.theta0(KIND_DNS)
+    tu[lay.phi_offset:lay.phi_offset + 9] = np.eye(3).reshape(-1) * 40.0
+    got = engine.estimate(KIND_DNS, tu, space=0, iterations=10, max_group_iters=1)
     assert got["status"][0] == 1 and np.isnan(got["ll"][0]) and np.isnan(got["theta_c"]).all()
 
 
@@ -143,8 +150,8 @@ def test_rolling_forecasts_driver(engine, tmp_path):
     tasks = np.arange(50, 57)
     np.testing.assert_array_equal(ex["tasks"], tasks)
     np.testing.assert_array_equal(ex["params"], mv["params"])  # both use the expanding sample (:165)
+    engine.set_panel(Y, mats)  # the moving-window forecasts left a window panel on the engine
     one = engine.estimate(KIND_DNS, th0, space=1, T_use=[53], iterations=25, max_group_iters=1)
-    engine.set_panel(Y, mats)
     np.testing.assert_array_equal(one["theta_c"][:, 0], ex["params"][:, 3])
     assert one["ll"][0] == ex["loss"][3]
     for i, task in enumerate(tasks):
