@@ -27,7 +27,7 @@ LANES = [1, 2, 4, 8, 16, 32, 64]
 def engine_default_lanes(B):
     """The launcher's own choice (yfm_tvl.hip: tvl_lanes_for) for N = 360."""
     L = 1
-    while L < min(64, -(-65536 // B)):
+    while L < min(64, -(-131072 // B)):
         L *= 2
     return L
 

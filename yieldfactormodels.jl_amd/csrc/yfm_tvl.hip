@@ -35,7 +35,7 @@ namespace yfm {
 namespace {
 
 constexpr int kTvlBlock = 256;
-constexpr int kTvlPre = 16;  // panel doubles prefetched per thread per chunk
+constexpr int kTvlPre = 8;  // panel doubles prefetched per thread per chunk (≤ 2 waves/SIMD of VGPRs)
 
 // x + (x of the partner lane) for the butterfly level `lvl` (partner distance 2^lvl,
 // every partner inside the same aligned group of 2^(lvl+1) lanes).
@@ -114,7 +114,7 @@ __global__ __launch_bounds__(256) void tvl_init_kernel(const double* __restrict_
 }
 
 template <int L, bool RECORD>
-__global__ __launch_bounds__(kTvlBlock) void tvl_loglik_kernel(
+__global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
     const double* __restrict__ rec, int B, const double* __restrict__ Y,
     const double* __restrict__ prep, int ldp, int np, int T, int N, int TC, const double* __restrict__ mats,
     int K, const double* __restrict__ gap_d, const int* __restrict__ gap_idx,
@@ -414,9 +414,11 @@ size_t tvl_scratch_bytes(int B) { return sizeof(double) * (size_t)kRecLen * (siz
 int tvl_max_n() { return (kTvlPre * kTvlBlock) - 1; }
 
 int tvl_lanes_for(int B, int N) {
-  // enough lanes for one wave per SIMD (256 CUs × 4 SIMDs × 64 lanes — the kernel's VGPR
-  // budget allows one), capped at a wave and at the maturity count rounded up to a power of two
-  long long want = (1024LL * 64 + B - 1) / (B > 0 ? B : 1);
+  // enough lanes for two waves per SIMD (256 CUs × 4 SIMDs × 2 × 64 lanes — the kernel is
+  // built for two; measured on MI355X at N = 360: B = 16,384 → L = 8 (5.98 ms vs 6.11 ms at
+  // L = 4), B = 65,536 → L = 2), capped at a wave and at the maturity count rounded up to a
+  // power of two
+  long long want = (2048LL * 64 + B - 1) / (B > 0 ? B : 1);
   int L = 1;
   while (L < want && L < 64) L <<= 1;
   int capN = 1;
