@@ -166,13 +166,14 @@ def cpu_baseline(w: Workload, seconds: float, gpu_out: np.ndarray):
 
 def pmc_traffic(kernel_substr: str):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 --pmc passes
-    (tools/profile_pmc.sh → profiles/<round>/pmc_summary.json): (FETCH_SIZE + WRITE_SIZE) KB × 1024, raw
-    (gfx950 FETCH_SIZE can under-count narrow reads by up to 2×, MI355X_MICROARCH.md §HBM)."""
+    (tools/profile_all.sh → profiles/<round>/**/pmc_summary.json), corrected as
+    MI355X_MICROARCH.md §HBM prescribes for gfx950: FETCH_SIZE counts half the bytes of wide
+    coalesced reads, so traffic = 2·FETCH_SIZE + WRITE_SIZE (both reported in KiB)."""
     for rnd in sorted((ROOT / "profiles").glob("r*/**/pmc_summary.json"), reverse=True):
         d = json.loads(rnd.read_text())
         for k, v in d.items():
             if kernel_substr in k and "FETCH_SIZE" in v and "WRITE_SIZE" in v:
-                return (v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024.0, str(rnd.relative_to(ROOT))
+                return (2.0 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024.0, str(rnd.relative_to(ROOT))
     return None, None
 
 
@@ -292,8 +293,7 @@ def main():
                        "parallelism": f"dp{world} (θ sharded, RCCL "
                                       f"{'all-gather of logliks + ' if w.gather else ''}argmax)", **w.extra},
             "roofline": {"bound": "fp64-valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic if kind == KIND_DNS else None,
-                         "traffic_source": traffic_src if kind == KIND_DNS else None,
+                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
                          "algorithmic_bytes": B * (P + 1) * 8 + T * (N + 4) * 8,
                          "kernel_ms": kernel_ms, "flops_per_eval": f_rank / max(B, 1),
                          "note": "achieved = SURVEY §8d algorithmic flops of this GPU's batch ÷ HIP-event time of "
