@@ -340,36 +340,50 @@ __device__ __forceinline__ double ldlt_solve(const double (&S)[M][M], double (&X
 }
 
 // β ← δ + Φ β_{t|t};  P ← Φ P_{t|t} Φ' + Q   (filter.jl:162-176).  Pf: upper triangle.
-template <int M, int LEAD>
-__device__ __forceinline__ void propagate_state(const Params<M, LEAD>& p, const double (&bf)[M], const double (&Pf)[M][M],
-                                          double (&beta)[M], double (&Pm)[M][M]) {
-#pragma unroll
-  for (int i = 0; i < M; ++i) {
-    double s = p.delta[i];
-#pragma unroll
-    for (int j = 0; j < M; ++j) s = fma(p.Phi[i][j], bf[j], s);
-    beta[i] = s;
-  }
+// `phi(i, j)` returns Φ_ij (registers, or LDS for the 5-factor kernel); each row of Φ is
+// read once per product so an LDS-backed Φ costs 2·M² reads per step.
+template <int M, class PhiF>
+__device__ __forceinline__ void propagate_state_f(PhiF phi, const double (&Q)[M][M], const double (&delta)[M],
+                                                  const double (&bf)[M], const double (&Pf)[M][M], double (&beta)[M],
+                                                  double (&Pm)[M][M]) {
   double A[M][M];
 #pragma unroll
-  for (int i = 0; i < M; ++i)
+  for (int i = 0; i < M; ++i) {
+    double f[M];
+#pragma unroll
+    for (int j = 0; j < M; ++j) f[j] = phi(i, j);
+    double s = delta[i];
+#pragma unroll
+    for (int j = 0; j < M; ++j) s = fma(f[j], bf[j], s);
+    beta[i] = s;
 #pragma unroll
     for (int j = 0; j < M; ++j) {
-      double s = 0.0;
+      double a = 0.0;
 #pragma unroll
-      for (int l = 0; l < M; ++l) s = fma(p.Phi[i][l], (l <= j) ? Pf[l][j] : Pf[j][l], s);
-      A[i][j] = s;
+      for (int l = 0; l < M; ++l) a = fma(f[l], (l <= j) ? Pf[l][j] : Pf[j][l], a);
+      A[i][j] = a;
     }
+  }
 #pragma unroll
-  for (int i = 0; i < M; ++i)
+  for (int j = 0; j < M; ++j) {
+    double f[M];
 #pragma unroll
-    for (int j = i; j < M; ++j) {
-      double s = p.Q[i][j];
+    for (int l = 0; l < M; ++l) f[l] = phi(j, l);
 #pragma unroll
-      for (int l = 0; l < M; ++l) s = fma(A[i][l], p.Phi[j][l], s);
+    for (int i = 0; i <= j; ++i) {
+      double s = Q[i][j];
+#pragma unroll
+      for (int l = 0; l < M; ++l) s = fma(A[i][l], f[l], s);
       Pm[i][j] = s;
       Pm[j][i] = s;
     }
+  }
+}
+
+template <int M, int LEAD>
+__device__ __forceinline__ void propagate_state(const Params<M, LEAD>& p, const double (&bf)[M], const double (&Pf)[M][M],
+                                                double (&beta)[M], double (&Pm)[M][M]) {
+  propagate_state_f<M>([&](int i, int j) { return p.Phi[i][j]; }, p.Q, p.delta, bf, Pf, beta, Pm);
 }
 
 // log|∏ d_t| accumulated as mantissa × 2^expo: one multiply and two frexp
