@@ -44,4 +44,52 @@ function loglik_batch(model, data::Matrix{Float64}, Θ::Matrix{Float64}; space =
         Θ::Ptr{Cdouble}, Cint(P)::Cint, Cint(B)::Cint, tu::Ptr{Cint}, out::Ptr{Cdouble})::Cint)
     out                                        # +loglik per column; -Inf / NaN as documented in yfm.h
 end
+ensure_panel!(model, data) = (c = ctx(); c.panel_id == objectid(data) ||
+                              set_panel!(c, data, Vector{Float64}(model.base.maturities)); c)
+tuse_ptr(T_use) = T_use === nothing ? C_NULL : pointer(T_use)
+
+"Batched predict (filter.jl:250-282) on hcat(data[:, 1:T_use[b]], NaN × (horizon−1)); arrays get a trailing batch axis."
+function predict_batch(model, data::Matrix{Float64}, Θc::Matrix{Float64}; horizon::Integer = 1,
+                       T_use::Union{Nothing,Vector{Cint}} = nothing)
+    c = ensure_panel!(model, data)
+    P, B = size(Θc)
+    N, T = size(data)
+    M = @ccall LIB.yfm_state_dim(kind(model)::Cint)::Cint
+    L = @ccall LIB.yfm_gamma_dim(kind(model)::Cint)::Cint
+    ncol = T + horizon - 1
+    preds, fl1, fl2 = (Array{Float64}(undef, N, ncol, B) for _ in 1:3)
+    factors = Array{Float64}(undef, M, ncol, B)
+    states = Array{Float64}(undef, L, ncol, B)
+    GC.@preserve Θc T_use preds fl1 fl2 factors states check(@ccall LIB.yfm_predict(c.ptr::Ptr{Cvoid},
+        kind(model)::Cint, CONSTRAINED::Cint, Θc::Ptr{Cdouble}, Cint(P)::Cint, Cint(B)::Cint, tuse_ptr(T_use)::Ptr{Cint},
+        Cint(horizon)::Cint, preds::Ptr{Cdouble}, factors::Ptr{Cdouble}, states::Ptr{Cdouble}, fl1::Ptr{Cdouble},
+        fl2::Ptr{Cdouble})::Cint)
+    (preds = preds, factors = factors, states = states, factor_loadings_1 = fl1, factor_loadings_2 = fl2)
+end
+
+"get_loss_array (filter.jl:211-247) per column of Θc: (T−1)×B, −Inf rows where the reference returns −Inf."
+function loss_array_batch(model, data::Matrix{Float64}, Θc::Matrix{Float64}; K::Integer = 1,
+                          T_use::Union{Nothing,Vector{Cint}} = nothing)
+    c = ensure_panel!(model, data)
+    P, B = size(Θc)
+    out = Matrix{Float64}(undef, size(data, 2) - 1, B)
+    GC.@preserve Θc T_use out check(@ccall LIB.yfm_loss_array(c.ptr::Ptr{Cvoid}, kind(model)::Cint,
+        CONSTRAINED::Cint, Θc::Ptr{Cdouble}, Cint(P)::Cint, Cint(B)::Cint, tuse_ptr(T_use)::Ptr{Cint}, Cint(K)::Cint,
+        out::Ptr{Cdouble})::Cint)
+    out
+end
+
+"R estimate_steps! chains (optimization.jl:137-312) batched on the device; starts Θ0c (constrained) on windows T_use."
+function estimate_batch(model, data::Matrix{Float64}, Θ0c::Matrix{Float64}; T_use = nothing, iterations = 500,
+                        g_tol = 1e-6, max_group_iters = 10, tol = 1e-8)
+    c = ensure_panel!(model, data)
+    P, R = size(Θ0c)
+    θc, p = Matrix{Float64}(undef, P, R), Matrix{Float64}(undef, P, R)
+    ll, status, nev = Vector{Float64}(undef, R), Vector{Cint}(undef, R), Ref{Clonglong}(0)
+    GC.@preserve Θ0c T_use θc p ll status check(@ccall LIB.yfm_estimate(c.ptr::Ptr{Cvoid}, kind(model)::Cint,
+        CONSTRAINED::Cint, Θ0c::Ptr{Cdouble}, Cint(P)::Cint, Cint(R)::Cint, tuse_ptr(T_use)::Ptr{Cint},
+        Cint(iterations)::Cint, Float64(g_tol)::Cdouble, Cint(max_group_iters)::Cint, Float64(tol)::Cdouble,
+        θc::Ptr{Cdouble}, p::Ptr{Cdouble}, ll::Ptr{Cdouble}, status::Ptr{Cint}, nev::Ptr{Clonglong})::Cint)
+    (theta_c = θc, p = p, ll = ll, status = status, n_evals = nev[])
+end
 end # module
