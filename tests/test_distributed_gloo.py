@@ -73,3 +73,53 @@ def test_sharded_equals_single_process(world):
     mp.spawn(_worker, args=(world, _free_port(), Theta, Y, mats, ret), nprocs=world, join=True)
     np.testing.assert_array_equal(ret["ll"], ref)
     assert ret["best"][0] == int(np.argmax(ref)) and ret["best"][1] == ref.max()
+
+
+def _argmax_worker(rank, world, port, ret):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # rank 0: [1, NaN, 5], rank 1: [5, 2] — the global maximum 5 is tied: lowest global index (2) wins
+    local = torch.tensor([[1.0, float("nan"), 5.0], [5.0, 2.0]][rank], dtype=torch.float64)
+    offset = [0, 3][rank]
+    dev = D.best_candidate_device(local, offset)
+    host = D.best_candidate(local, offset)
+    allv = D.gather_logliks(local, [3, 2])
+    if rank == 0:
+        ret["dev"] = dev.tolist()
+        ret["host"] = host
+        ret["all"] = allv.tolist()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_argmax_reduce_ties_nan_and_ragged_gather():
+    """The bench's device-side argmax (yfm_amd.distributed.best_candidate_device) and the host
+    reduce agree: NaN (init throw) never wins, ties go to the lowest global index; the ragged
+    all-gather returns every rank's logliks in global order."""
+    mgr = mp.Manager()
+    ret = mgr.dict()
+    mp.spawn(_argmax_worker, args=(2, _free_port(), ret), nprocs=2, join=True)
+    assert ret["dev"] == [5.0, 2.0] and ret["host"] == (2, 5.0)
+    assert np.array_equal(np.array(ret["all"]), np.array([1.0, np.nan, 5.0, 5.0, 2.0]), equal_nan=True)
+
+
+@pytest.mark.parametrize("config", [4, 5])
+def test_bench_sharding_covers_every_unit_once(config):
+    """bench.py's per-rank workloads (configs 4 and 5, strong scaling) partition the global job:
+    every (window, θ) pair / candidate is evaluated by exactly one of N ranks, N = 1, 2, 4, 8."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+    import bench
+    for world in (1, 2, 4, 8):
+        seen = []
+        sizes = []
+        for rank in range(world):
+            w = bench.make_workload(config, world, rank, 60, 16)
+            sizes.append(w.Theta.shape[1])
+            if config == 4:
+                # (window length, θ column) pairs; θ columns repeat the same 16 starts per window
+                seen += list(zip(w.T_use.tolist(), map(tuple, np.round(w.Theta.T, 12).tolist())))
+            else:
+                seen += list(range(w.extra["offset"], w.extra["offset"] + w.Theta.shape[1]))
+        assert len(seen) == len(set(seen)) == w.global_batch
+        assert max(sizes) - min(sizes) <= (60 if config == 4 else 1)
