@@ -1,0 +1,60 @@
+"""GPU parity of the fixed-loading models at maturity counts beyond the per-lane kernel
+(N > 64 → yfm_group.hip: one filter per lane group, DPP reductions), e.g. the 360 monthly
+maturities of config 3's panel — vs the NumPy oracle (dense N×N LAPACK path) and the C oracle.
+Tolerance: the parity rule of test_gpu_parity.assert_parity (1e-9 relative, adjudicated by the
+long-double truth proxy where the dense oracle is itself further than that from exact
+arithmetic), normwise on the state trajectories."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from oracle import kalman_oracle as O
+from oracle.kalman_ld import loglik_ld
+from test_gpu_parity import assert_ll_close, assert_parity
+from yfm_amd import KIND_DNS, KIND_GNS
+from yfm_amd import synthetic as S
+from yfm_amd.params import state_dim, transform_params
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("kind,N,T", [(KIND_DNS, 65, 40), (KIND_DNS, 360, 30), (KIND_DNS, 1000, 12),
+                                      (KIND_GNS, 90, 30), (KIND_GNS, 512, 12)])
+def test_large_n_loglik_vs_oracle(engine, kind, N, T):
+    mats = np.arange(1, N + 1, dtype=np.float64) * (360.0 / N)
+    Y = S.simulate_panel(kind, T, maturities=mats)
+    Th = S.theta_batch(kind, 12, seed=71 + N, bad_frac=0.0, scale=0.05)
+    engine.set_panel(Y, mats)
+    got = engine.loglik(kind, Th)
+    ref = np.array([O.loglik(kind, mats, state_dim(kind), Y, Th[:, b]) for b in range(12)])
+    # the dense N×N FP64 oracle can itself be ~1e-9 from exact arithmetic at N = 360: the
+    # long-double proxy adjudicates (assert_parity: within 1e-9 of the oracle, or closer to the
+    # truth than the oracle is)
+    assert_parity(got, ref, loglik_ld(kind, mats, Y, Th))
+
+
+def test_large_n_windows_nan_states_and_predict(engine):
+    """N = 360: T_use windows, a NaN column, the filtered-state trajectory and predict."""
+    N, T = 360, 40
+    mats = np.arange(1, N + 1, dtype=np.float64)
+    Y = S.simulate_panel(KIND_DNS, T, maturities=mats).copy(order="F")
+    Y[:, 17] = np.nan
+    Th = transform_params(KIND_DNS, S.theta_batch(KIND_DNS, 4, seed=73, bad_frac=0.0, scale=0.05))
+    tu = np.array([40, 30, 18, 3], dtype=np.int32)
+    engine.set_panel(Y, mats)
+    got = engine.loglik(KIND_DNS, Th, space=1, T_use=tu)
+    ref = np.array([O.loglik(KIND_DNS, mats, 3, Y[:, :tu[b]], Th[:, b], space=1) for b in range(4)])
+    assert_ll_close(got, ref)
+    ll, beta, P = engine.filter_states(KIND_DNS, Th[:, :2], space=1)
+    for b in range(2):
+        rec = []
+        O.loglik(KIND_DNS, mats, 3, Y, Th[:, b], space=1, record=rec)
+        rb = np.stack([r[0] for r in rec], axis=1)
+        assert np.abs(beta[..., b] - rb).max() / np.abs(rb).max() <= 1e-9
+    r = engine.predict(KIND_DNS, Th[:, :1], space=1, horizon=4)
+    s = O.KalmanState.fresh(KIND_DNS, mats, 3)
+    O.set_params(s, Th[:, 0])
+    ro = O.predict(s, O.pad_nan(Y, 4))
+    for k in ("preds", "factors", "factor_loadings_1"):
+        assert np.abs(r[k][..., 0] - ro[k]).max() / np.abs(ro[k]).max() <= 1e-9, k

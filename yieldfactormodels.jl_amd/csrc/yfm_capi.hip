@@ -108,8 +108,9 @@ int check_batch(yfm_ctx* ctx, int kind, int space, int P, int B) {
       return set_error(YFM_EUNSUPPORTED, "N = %d maturities exceeds the TVλ kernel's %d", ctx->N, yfm::tvl_max_n());
     return YFM_OK;
   }
-  if (yfm::fixedz_np_for(ctx->N) < 0)
-    return set_error(YFM_EUNSUPPORTED, "N = %d maturities exceeds the fixed-loading kernel's 64", ctx->N);
+  if (yfm::fixedz_np_for(ctx->N) < 0 && ctx->N > yfm::group_max_n(kind))
+    return set_error(YFM_EUNSUPPORTED, "N = %d maturities exceeds the fixed-loading kernels' %d", ctx->N,
+                     yfm::group_max_n(kind));
   return YFM_OK;
 }
 
@@ -208,7 +209,8 @@ int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int 
     if (int r = tvl_gaps(ctx, lanes, g)) return r;
     e = yfm::launch_tvl(a, g, lanes);
   } else {
-    e = yfm::launch_fixedz(kind, a);
+    // N ≤ 64: one filter per lane (MFMA Z'y); larger N: one filter per lane group
+    e = yfm::fixedz_np_for(ctx->N) > 0 ? yfm::launch_fixedz(kind, a) : yfm::launch_fixedz_group(kind, a);
   }
   if (e != hipSuccess) return set_error(YFM_EHIP, "kernel launch: %s", hipGetErrorString(e));
   return YFM_OK;

@@ -25,6 +25,10 @@ struct LaunchArgs {
 // padded maturity count NP the fixed-loading kernel is instantiated for (-1: none)
 int fixedz_np_for(int N);
 hipError_t launch_fixedz(int kind, const LaunchArgs& a);
+// fixed-loading models with N beyond the per-lane kernel (yfm_group.hip): filter per lane group
+int group_max_n(int kind);
+int group_lanes_for(int kind, int N);
+hipError_t launch_fixedz_group(int kind, const LaunchArgs& a);
 // TVλ EKF kernel (yfm_tvl.hip): lanes per filter for a batch, largest N, launcher
 int tvl_lanes_for(int B, int N);
 int tvl_max_n();

@@ -27,7 +27,7 @@
 // Panel layout in HBM (built by prep_panel_kernel from the caller's N×T
 // column-major matrix): T columns of LDP = NP + 4 doubles —
 //   [ ỹ_0 … ỹ_{N-1}, 0 … 0 (to NP), ȳ, ỹ'ỹ, isnan(any y), y'y ].
-#include "yfm_device.hpp"
+#include "yfm_fixedz.hpp"
 
 namespace yfm {
 
@@ -84,63 +84,6 @@ __device__ __forceinline__ void dot_zt(const double* __restrict__ col, const dou
   }
 #pragma unroll
   for (int cz = 0; cz < NZ; ++cz) zt[cz] = a[cz][0] + a[cz][1];
-}
-
-// Collapsed-form measurement update (see the header): returns det S and q = v'F⁻¹v,
-// writes β_{t|t} (bf) and the upper triangle of P_{t|t} (Pf).
-template <int M>
-__device__ __forceinline__ void collapsed_update(const double (&zt)[M - 1], double ybar, double ytt,
-                                                 const double (&R)[M][M], double rsig2, const double (&beta)[M],
-                                                 const double (&Pm)[M][M], double (&bf)[M], double (&Pf)[M][M],
-                                                 double& det, double& q) {
-  double zs[M - 1];
-#pragma unroll
-  for (int j = 0; j < M - 1; ++j) zs[j] = zt[j] * rsig2;
-  double ch[M];  // ĉ = G⁻¹(0, z̃) (= R/σ² · (0, z̃))
-#pragma unroll
-  for (int i = 0; i < M; ++i) {
-    double s = 0.0;
-#pragma unroll
-    for (int j = 1; j < M; ++j) s = fma(R[i][j], zs[j - 1], s);
-    ch[i] = s;
-  }
-  double rr = ytt;  // ‖ỹ − Zĉ‖² = ỹ'ỹ − z̃'ĉ
-#pragma unroll
-  for (int j = 1; j < M; ++j) rr = fma(-zt[j - 1], ch[j], rr);
-  ch[0] += ybar;
-  double S[M][M];
-  double X[M][M + 1];  // [c | R] → [S⁻¹c | S⁻¹R]
-  double c[M];
-#pragma unroll
-  for (int i = 0; i < M; ++i) {
-    c[i] = ch[i] - beta[i];
-#pragma unroll
-    for (int j = 0; j <= i; ++j) S[i][j] = Pm[i][j] + R[i][j];  // LDLᵀ reads the lower triangle only
-#pragma unroll
-    for (int j = 0; j < M; ++j) X[i][j + 1] = R[i][j];
-    X[i][0] = c[i];
-  }
-  det = ldlt_solve<M, M + 1>(S, X);
-  double cx = 0.0;
-#pragma unroll
-  for (int i = 0; i < M; ++i) cx = fma(c[i], X[i][0], cx);
-  q = fma(rr, rsig2, cx);
-#pragma unroll
-  for (int i = 0; i < M; ++i) {
-    double s = beta[i];
-#pragma unroll
-    for (int k = 0; k < M; ++k) s = fma(Pm[i][k], X[k][0], s);
-    bf[i] = s;
-  }
-#pragma unroll
-  for (int i = 0; i < M; ++i)
-#pragma unroll
-    for (int j = i; j < M; ++j) {
-      double s = 0.0;
-#pragma unroll
-      for (int k = 0; k < M; ++k) s = fma(Pm[i][k], X[k][j + 1], s);
-      Pf[i][j] = s;
-    }
 }
 
 typedef double yfm_double4 __attribute__((ext_vector_type(4)));
@@ -270,55 +213,16 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     }
   }
 
-  const double sigma2 = p.sigma2;
-  const double rsig2 = 1.0 / sigma2;
-
-  // G⁻¹ (pivoted elimination) and log det G; decide collapsed vs capacitance per lane.
-  double R[M][M];
-  double logdetG = 0.0;
-  bool collapsed;
-  {
-    double A[M][M], X[M][M];
-    double hadamard = 1.0;
-#pragma unroll
-    for (int i = 0; i < M; ++i) {
-      hadamard *= G[i][i];
-#pragma unroll
-      for (int j = 0; j < M; ++j) {
-        A[i][j] = G[i][j];
-        X[i][j] = (i == j) ? 1.0 : 0.0;
-      }
-    }
-    const bool ok = gauss_solve<M, M>(A, X);
-    double detG = 1.0;
-#pragma unroll
-    for (int i = 0; i < M; ++i) detG *= A[i][i];
-    detG = fabs(detG);
-    // Z'Z must be numerically nonsingular: det / ∏ diag (Hadamard ratio, ≤ 1).
-    collapsed = ok && (N >= M) && (detG > 1e-13 * hadamard);
-    logdetG = collapsed ? log(detG) : 0.0;
-#pragma unroll
-    for (int i = 0; i < M; ++i)
-#pragma unroll
-      for (int j = 0; j < M; ++j) R[i][j] = collapsed ? sigma2 * 0.5 * (X[i][j] + X[j][i]) : G[i][j];
-  }
-  // From here R holds σ²(Z'Z)⁻¹ on collapsed lanes and G = Z'Z on capacitance lanes (one
-  // register image for both: each lane only ever needs one of them).
-
-  double beta[M], Pm[M][M];
-  const bool init_ok = init_state<M, LEAD>(p, beta, Pm);
-
-  LogDetAcc ld;
-  double sumq = 0.0;
-  bool neg = false;
-  double last_det = 0.0, last_q = 0.0;  // fresh model: F = 0, F⁻¹ = 0, v = 0 (kalmanbasemodel.jl:65-67)
+  FixedZFilter<M, LEAD, RECORD> f;
+  f.p = p;
+  f.setup(G, N);
 
   // wave-uniform facts for the fast path
   int wmin = live ? my_data : 0x7fffffff;
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) wmin = min(wmin, __shfl_xor(wmin, off));
   const int wave_min_data = __builtin_amdgcn_readfirstlane(wmin);
-  const bool wave_all_collapsed = __ballot(!collapsed) == 0ull;
+  const bool wave_all_collapsed = __ballot(!f.collapsed) == 0ull;
 
   __syncthreads();
   const int nsteps = max(s_nobs_max, 0);
@@ -355,109 +259,11 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   // one filter step given z̃_t (zc), (ȳ, ỹ'ỹ) and (nanflag, y'y) of column t
   auto do_step = [&](int t, const double (&zc)[NZ], double2 yb_c, double2 meta_c) {
     const bool fast = (t >= 1) && (meta_c.x == 0.0) && (t < wave_min_data) && wave_all_collapsed;
-    if (fast) {
-      double bf[M], Pf[M][M], det, q;
-      collapsed_update<M>(zc, yb_c.x, yb_c.y, R, rsig2, beta, Pm, bf, Pf, det, q);
-      // (a singular F at t ≥ 2 makes the loglik −Inf whatever the state; trajectories skip the update)
-      if (!RECORD || det != 0.0) propagate_state<M, LEAD>(p, bf, Pf, beta, Pm);
-      last_det = det;
-      last_q = q;
-      ld.mul(det);
-      sumq += q;
-      neg = neg || (det < 0.0);
-      return;
-    }
-    const bool act = t < my_steps;
-    const bool acc = t >= 1;  // Julia t > 1 (filter.jl:194)
-    if (!act) return;
-    if (meta_c.x != 0.0 || t >= my_data) {
-      // NaN column: prediction only (filter.jl:126-140); F, v stale → the loglik
-      // re-adds the previous term (filter.jl:195 reads base.F / base.v unchanged).
-      double Pf[M][M];
-#pragma unroll
-      for (int i = 0; i < M; ++i)
-#pragma unroll
-        for (int j = i; j < M; ++j) Pf[i][j] = Pm[i][j];
-      double bf[M];
-#pragma unroll
-      for (int i = 0; i < M; ++i) bf[i] = beta[i];
-      propagate_state<M, LEAD>(p, bf, Pf, beta, Pm);
-      if (acc) {
-        ld.mul(last_det);
-        sumq += last_q;
-        neg = neg || (last_det < 0.0);
-      }
-      return;
-    }
-    double det, q;
-    double bf[M];
-    double Pf[M][M];
-    if (collapsed) {
-      collapsed_update<M>(zc, yb_c.x, yb_c.y, R, rsig2, beta, Pm, bf, Pf, det, q);
-    } else {
-      // capacitance form on uncentered sums: Z'y = (Nȳ, z̃ + ȳ G[1:,0]), y'y
-      double zy[M];
-      zy[0] = (double)N * yb_c.x;
-#pragma unroll
-      for (int j = 1; j < M; ++j) zy[j] = fma(yb_c.x, R[j][0], zc[j - 1]);
-      double u[M];
-      double bgb = 0.0, bzy = 0.0;
-#pragma unroll
-      for (int i = 0; i < M; ++i) {
-        double g = 0.0;
-#pragma unroll
-        for (int j = 0; j < M; ++j) g = fma(R[i][j], beta[j], g);
-        u[i] = zy[i] - g;
-        bgb = fma(beta[i], g, bgb);
-        bzy = fma(beta[i], zy[i], bzy);
-      }
-      const double vv = fma(-2.0, bzy, meta_c.y) + bgb;
-      double W[M][M];
-      Capacitance<M>::solve(Pm, R, sigma2, W, det);
-#pragma unroll
-      for (int i = 0; i < M; ++i)
-#pragma unroll
-        for (int j = 0; j < i; ++j) W[i][j] = W[j][i];
-      double uk = 0.0;
-#pragma unroll
-      for (int i = 0; i < M; ++i) {
-        double s = 0.0;
-#pragma unroll
-        for (int j = 0; j < M; ++j) s = fma(W[i][j], u[j], s);
-        bf[i] = beta[i] + s;
-        uk = fma(u[i], s, uk);
-      }
-      q = (vv - uk) * rsig2;
-#pragma unroll
-      for (int i = 0; i < M; ++i)
-#pragma unroll
-        for (int j = i; j < M; ++j) Pf[i][j] = sigma2 * W[i][j];
-    }
-    const bool upd = det != 0.0;  // inv(F) threw: return without the update (filter.jl:151-154)
-    if (upd) propagate_state<M, LEAD>(p, bf, Pf, beta, Pm);
-    last_det = det;
-    last_q = upd ? q : __builtin_nan("");
-    if (acc) {
-      ld.mul(det);
-      sumq += last_q;
-      neg = neg || (det < 0.0);
-    }
+    f.step(t, zc, yb_c, meta_c, fast, my_steps, my_data);
   };
   auto record = [&](int t) {
     if constexpr (RECORD) {
-      // the state after step t, into slot t − max(0, my_steps − rec_len) (the last rec_len steps)
-      const int slot = t - max(0, my_steps - rec_len);
-      if (live && t < my_steps && slot >= 0) {
-        const size_t o = (size_t)b * (size_t)rec_len + slot;
-#pragma unroll
-        for (int i = 0; i < M; ++i) rec_beta[o * M + i] = beta[i];
-        if (rec_P) {
-#pragma unroll
-          for (int j = 0; j < M; ++j)
-#pragma unroll
-            for (int i = 0; i < M; ++i) rec_P[o * M * M + j * M + i] = Pm[i][j];
-        }
-      }
+      if (live) f.record(t, b, my_steps, rec_len, rec_beta, rec_P);
     }
   };
   auto rotate = [&](int t) {  // after step t: if chunk c = t / kTC is done, its buffer takes chunk c + 2
@@ -559,23 +365,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   }
 
   if (!live) return;
-  double ll;
-  if (!init_ok) {
-    ll = __builtin_nan("");  // the reference throws from initialize_filter
-    atomicAdd(&flags[0], 1u);
-  } else {
-    const int nterms = max(nobs - 2, 0);
-    if (nterms == 0) {
-      ll = 0.0;
-    } else {
-      const double per_term = (double)(N - M) * log(sigma2) + logdetG + (double)N * kLog2Pi;
-      ll = -0.5 * ((double)nterms * per_term + ld.log_value() + sumq);
-    }
-    if (neg || !isfinite(ll)) {  // DomainError / non-finite → -Inf (filter.jl:197-204)
-      ll = -__builtin_inf();
-      atomicAdd(&flags[1], 1u);
-    }
-  }
+  const double ll = f.loglik(nobs, flags);
   out[b] = ll;
 }
 

@@ -37,42 +37,6 @@ namespace {
 constexpr int kTvlBlock = 256;
 constexpr int kTvlPre = 8;  // panel doubles prefetched per thread per chunk (≤ 2 waves/SIMD of VGPRs)
 
-// x + (x of the partner lane) for the butterfly level `lvl` (partner distance 2^lvl,
-// every partner inside the same aligned group of 2^(lvl+1) lanes).
-template <int LVL>
-__device__ __forceinline__ double group_level_sum(double x) {
-  const int lo = __double2loint(x), hi = __double2hiint(x);
-  if constexpr (LVL == 0 || LVL == 1 || LVL == 2 || LVL == 3) {
-    // quad_perm xor1 / xor2, row_half_mirror, row_mirror
-    constexpr int ctrl = LVL == 0 ? 0xB1 : LVL == 1 ? 0x4E : LVL == 2 ? 0x141 : 0x140;
-    const int plo = __builtin_amdgcn_update_dpp(0, lo, ctrl, 0xf, 0xf, false);
-    const int phi = __builtin_amdgcn_update_dpp(0, hi, ctrl, 0xf, 0xf, false);
-    return x + __hiloint2double(phi, plo);
-  } else if constexpr (LVL == 4) {
-    // rows (0,1), (2,3): vdst' = [r0 r0 r2 r2], src' = [r1 r1 r3 r3]
-    const auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-    const auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-    return __hiloint2double(rh[0], rl[0]) + __hiloint2double(rh[1], rl[1]);
-  } else {
-    // halves: vdst' = [lo lo], src' = [hi hi]
-    const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
-    const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-    return __hiloint2double(rh[0], rl[0]) + __hiloint2double(rh[1], rl[1]);
-  }
-}
-
-// Sum over the aligned group of L lanes; every lane of the group receives the total.
-template <int L>
-__device__ __forceinline__ double group_sum(double x) {
-  if constexpr (L >= 2) x = group_level_sum<0>(x);
-  if constexpr (L >= 4) x = group_level_sum<1>(x);
-  if constexpr (L >= 8) x = group_level_sum<2>(x);
-  if constexpr (L >= 16) x = group_level_sum<3>(x);
-  if constexpr (L >= 32) x = group_level_sum<4>(x);
-  if constexpr (L >= 64) x = group_level_sum<5>(x);
-  return x;
-}
-
 }  // namespace
 
 // Sufficient statistics of one EKF step, indices into the accumulator array.
