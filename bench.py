@@ -158,9 +158,19 @@ def cpu_baseline(w: Workload, seconds: float, gpu_out: np.ndarray):
         parity.update(truth_subset=k, gpu_vs_truth_max_rel=float(e_gpu.max()) if e_gpu.size else 0.0,
                       oracle_vs_truth_max_rel=float(e_ref.max()) if e_ref.size else 0.0)
     win = "" if w.T_use is None else " with the workload's window lengths"
+    # config 1 (BASELINE.json configs[0]): one θ, single thread — the reference's own CPU case
+    th0 = np.asfortranarray(w.Theta[:, :1])
+    one = np.empty(1)
+    n1, t1 = 0, time.perf_counter()
+    while n1 < 3 or (time.perf_counter() - t1 < 2.0 and n1 < 200):
+        lib.yfm_oracle_loglik(w.kind, 0, Yf.ctypes.data_as(Dp), N, T, w.mats.ctypes.data_as(Dp), th0.ctypes.data_as(Dp),
+                              P, 1, None, one.ctypes.data_as(Dp), 1)
+        n1 += 1
+    ms1 = 1e3 * (time.perf_counter() - t1) / n1
     return {"value": done / dt if dt > 0 else 0.0, "unit": "evals/s", "cores": threads, "kind": "port",
             "sample": f"{done} of the benchmark's θ (T={T}, N={N}){win} in {dt:.1f} s, dense N×N getrf+getri + "
                       f"logdet LU per step (oracle/yfm_oracle.c, -O3, OpenMP {threads} threads)",
+            "single_theta_1_thread": {"ms_per_eval": ms1, "evals_per_s": 1e3 / ms1, "evals_timed": n1},
             "parity": parity}
 
 
