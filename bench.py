@@ -227,48 +227,66 @@ def main():
     counts = w.counts or [B] * world
     stream = torch.cuda.current_stream(dev)
 
-    def step():
-        eng.loglik_device(kind, d_th.data_ptr(), P, B, d_out.data_ptr(), space=0,
-                          d_T_use=d_tu.data_ptr() if d_tu is not None else None, stream=stream.cuda_stream)
-        if world > 1:  # RCCL over xGMI: gather logliks and/or reduce the best candidate
-            if w.gather:
-                D.gather_logliks(d_out, counts)
-            D.best_candidate_device(d_out, offset)
+    # N > 1: the kernel runs on a compute stream into one of two output buffers while the
+    # previous step's collectives (RCCL all-gather + argmax) run on torch's stream — step k's
+    # gather overlaps step k+1's filter.  Events order buffer reuse both ways.
+    comp = torch.cuda.Stream(dev) if world > 1 else stream
+    outs = [d_out, torch.empty_like(d_out)] if world > 1 else [d_out]
+    k_done = [torch.cuda.Event() for _ in outs]
+    c_done = [torch.cuda.Event() for _ in outs]
+    k_times = []  # (start, end) HIP events around each timed launch, on the launch stream
+    timing = [False]
+    it = [0]
 
+    def step():
+        i = it[0] % len(outs)
+        it[0] += 1
+        o = outs[i]
+        if world > 1:
+            comp.wait_event(c_done[i])  # the collective that last read buffer i has finished
+        if timing[0]:
+            ks, ke = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ks.record(comp)
+        eng.loglik_device(kind, d_th.data_ptr(), P, B, o.data_ptr(), space=0,
+                          d_T_use=d_tu.data_ptr() if d_tu is not None else None, stream=comp.cuda_stream)
+        if timing[0]:
+            ke.record(comp)
+            k_times.append((ks, ke))
+        if world > 1:  # RCCL over xGMI: gather logliks and/or reduce the best candidate
+            k_done[i].record(comp)
+            stream.wait_event(k_done[i])
+            if w.gather:
+                D.gather_logliks(o, counts)
+            D.best_candidate_device(o, offset)
+            c_done[i].record(stream)
+
+    for e in c_done:
+        e.record(stream)
     for _ in range(args.warmup):
         step()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    timing[0] = True
     t0 = time.perf_counter()
     ev0.record(stream)
+    comp.wait_stream(stream)
     for _ in range(args.steps):
         step()
+    stream.wait_stream(comp)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
-    ev_ms = ev0.elapsed_time(ev1) / args.steps
+    timing[0] = False
     if world > 1:
         t = torch.tensor([wall], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
-
-    # kernel-only time of one batch (no collectives) on the library's stream, for the roofline
-    if world > 1:
-        torch.cuda.synchronize(dev)
-        k0, k1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        k0.record(stream)
-        for _ in range(max(1, min(args.steps, 5))):
-            eng.loglik_device(kind, d_th.data_ptr(), P, B, d_out.data_ptr(), space=0,
-                              d_T_use=d_tu.data_ptr() if d_tu is not None else None, stream=stream.cuda_stream)
-        k1.record(stream)
-        torch.cuda.synchronize(dev)
-        kernel_ms = k0.elapsed_time(k1) / max(1, min(args.steps, 5))
-    else:
-        kernel_ms = ev_ms
+    # kernel time of one batch: HIP events around each launch in the timed region, on its stream
+    kernel_ms = float(np.mean([ks.elapsed_time(ke) for ks, ke in k_times]))
 
     ms_per_step = 1e3 * wall / args.steps
     value = w.global_batch / (wall / args.steps)
