@@ -1,0 +1,85 @@
+"""Rolling re-estimation throughput — the reference's own printed number ("average seconds per
+task", forecasting.jl:144-189): every forecast origin of config 4 (expanding windows
+T_w = 361..600 of the T = 600, N = 30 DNS panel) re-estimated with estimate_steps!'s defaults
+(NelderMead opt1: 500 iterations, g_tol 1e-6; max_group_iters 10, tol 1e-8), all windows as ONE
+batched yfm_estimate call, next to ONE window's chain on the faithful CPU path (oracle/optim_nm.py
+driving the dense C restatement oracle/yfm_oracle.c, single thread — what one reference process
+does per task).
+
+    python tools/bench_estimate.py [--windows 240] [--cpu-window 480]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import math
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "yieldfactormodels.jl_amd"))
+sys.path.insert(0, str(ROOT))
+
+from oracle import optim_nm as NM  # noqa: E402  (CPU reference leg only)
+from yfm_amd import KIND_DNS, Engine  # noqa: E402
+from yfm_amd import synthetic as S  # noqa: E402
+from yfm_amd.params import transform_params, untransform_params  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--windows", type=int, default=240)
+    ap.add_argument("--cpu-window", type=int, default=480)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+    torch.cuda.set_device(0)
+    mats = S.maturities_30()
+    Y = S.simulate_panel(KIND_DNS, 600)
+    th0 = S.theta0_constrained(KIND_DNS)
+    wins = np.arange(601 - args.windows, 601, dtype=np.int32)
+    eng = Engine(0)
+    eng.set_panel(Y, mats)
+    Th0 = np.repeat(th0[:, None], len(wins), axis=1)
+    eng.estimate(KIND_DNS, Th0[:, :2], space=1, T_use=wins[:2], iterations=5, max_group_iters=1)  # warm up
+    t0 = time.perf_counter()
+    r = eng.estimate(KIND_DNS, Th0, space=1, T_use=wins)
+    gpu_s = time.perf_counter() - t0
+    out = {"metric": "rolling re-estimation (estimate_steps!, NelderMead opt1), DNS T≤600 N=30",
+           "windows": int(len(wins)), "gpu_seconds_all_windows": gpu_s, "gpu_seconds_per_task": gpu_s / len(wins),
+           "gpu_objective_evals": int(r["n_evals"]), "status_counts": np.bincount(r["status"], minlength=3).tolist()}
+    if not args.no_cpu:
+        lib = ctypes.CDLL(str(ROOT / "oracle" / "libyfm_oracle.so"))
+        D = ctypes.POINTER(ctypes.c_double)
+        Tw = int(args.cpu_window)
+        Yw = np.asfortranarray(Y[:, :Tw])
+        calls = [0]
+
+        def f(theta):
+            calls[0] += 1
+            th = np.ascontiguousarray(theta, dtype=np.float64)
+            o = np.empty(1)
+            lib.yfm_oracle_loglik(KIND_DNS, 0, Yw.ctypes.data_as(D), 30, Tw, mats.ctypes.data_as(D),
+                                  th.ctypes.data_as(D), 20, 1, None, o.ctypes.data_as(D), 1)
+            if math.isnan(o[0]):
+                raise NM.InitThrow()
+            return -o[0]
+
+        t0 = time.perf_counter()
+        ref = NM.estimate_steps(f, th0, transform=lambda x: transform_params(KIND_DNS, x),
+                                untransform=lambda x: untransform_params(KIND_DNS, x))
+        cpu_s = time.perf_counter() - t0
+        k = int(np.flatnonzero(wins == Tw)[0])
+        out.update({"cpu_window": Tw, "cpu_seconds_one_task": cpu_s, "cpu_objective_evals": calls[0],
+                    "cpu_threads": 1, "cpu_kind": "port (oracle/optim_nm.py + oracle/yfm_oracle.c)",
+                    "gpu_vs_cpu_ll_rel": abs(r["ll"][k] - ref.ll) / abs(ref.ll),
+                    "speedup_per_task": cpu_s / (gpu_s / len(wins))})
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
