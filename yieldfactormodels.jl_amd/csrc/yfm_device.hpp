@@ -339,6 +339,56 @@ __device__ __forceinline__ double ldlt_solve(const double (&S)[M][M], double (&X
   return det;
 }
 
+// The same LDLᵀ split in two, so callers can stream the right-hand sides one at a time
+// (fewer live registers; per-element arithmetic identical to ldlt_solve).
+template <int M>
+struct LDLT {
+  double L[M][M];  // strictly lower part used
+  double rd[M];    // 1 / d_i
+  __device__ __forceinline__ double factor(const double (&S)[M][M]) {
+    double a[M][M];
+    double d[M];
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      double dj = S[j][j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) dj = fma(-a[j][k], L[j][k], dj);
+      d[j] = dj;
+      rd[j] = rcp_nr(dj);
+#pragma unroll
+      for (int i = j + 1; i < M; ++i) {
+        double s = S[i][j];
+#pragma unroll
+        for (int k = 0; k < j; ++k) s = fma(-a[i][k], L[j][k], s);
+        a[i][j] = s;
+        L[i][j] = s * rd[j];
+      }
+    }
+    double det = d[0];
+#pragma unroll
+    for (int i = 1; i < M; ++i) det *= d[i];
+    return det;
+  }
+  __device__ __forceinline__ void solve(double (&x)[M]) const {
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      double s = x[i];
+#pragma unroll
+      for (int k = 0; k < i; ++k) s = fma(-L[i][k], x[k], s);
+      x[i] = s;
+    }
+#pragma unroll
+    for (int i = 0; i < M; ++i) x[i] *= rd[i];
+#pragma unroll
+    for (int i = M - 1; i >= 0; --i) {
+      double s = x[i];
+#pragma unroll
+      for (int k = i + 1; k < M; ++k) s = fma(-L[k][i], x[k], s);
+      x[i] = s;
+    }
+  }
+};
+
 // β ← δ + Φ β_{t|t};  P ← Φ P_{t|t} Φ' + Q   (filter.jl:162-176).  Pf: upper triangle.
 // `phi(i, j)` returns Φ_ij (registers, or LDS for the 5-factor kernel); each row of Φ is
 // read once per product so an LDS-backed Φ costs 2·M² reads per step.

@@ -33,38 +33,45 @@ __device__ __forceinline__ void collapsed_update(const double (&zt)[M - 1], doub
   for (int j = 1; j < M; ++j) rr = fma(-zt[j - 1], ch[j], rr);
   ch[0] += ybar;
   double S[M][M];
-  double X[M][M + 1];  // [c | R] → [S⁻¹c | S⁻¹R]
   double c[M];
 #pragma unroll
   for (int i = 0; i < M; ++i) {
     c[i] = ch[i] - beta[i];
 #pragma unroll
     for (int j = 0; j <= i; ++j) S[i][j] = Pm[i][j] + R[i][j];  // LDLᵀ reads the lower triangle only
-#pragma unroll
-    for (int j = 0; j < M; ++j) X[i][j + 1] = R[i][j];
-    X[i][0] = c[i];
   }
-  det = ldlt_solve<M, M + 1>(S, X);
+  LDLT<M> f;
+  det = f.factor(S);
+  // right-hand sides streamed one at a time: x = S⁻¹c, then S⁻¹R column by column
+  double x[M];
+#pragma unroll
+  for (int i = 0; i < M; ++i) x[i] = c[i];
+  f.solve(x);
   double cx = 0.0;
 #pragma unroll
-  for (int i = 0; i < M; ++i) cx = fma(c[i], X[i][0], cx);
+  for (int i = 0; i < M; ++i) cx = fma(c[i], x[i], cx);
   q = fma(rr, rsig2, cx);
 #pragma unroll
   for (int i = 0; i < M; ++i) {
     double s = beta[i];
 #pragma unroll
-    for (int k = 0; k < M; ++k) s = fma(Pm[i][k], X[k][0], s);
+    for (int k = 0; k < M; ++k) s = fma(Pm[i][k], x[k], s);
     bf[i] = s;
   }
 #pragma unroll
-  for (int i = 0; i < M; ++i)
+  for (int j = 0; j < M; ++j) {
+    double xj[M];
 #pragma unroll
-    for (int j = i; j < M; ++j) {
+    for (int i = 0; i < M; ++i) xj[i] = R[i][j];
+    f.solve(xj);
+#pragma unroll
+    for (int i = 0; i <= j; ++i) {
       double s = 0.0;
 #pragma unroll
-      for (int k = 0; k < M; ++k) s = fma(Pm[i][k], X[k][j + 1], s);
+      for (int k = 0; k < M; ++k) s = fma(Pm[i][k], xj[k], s);
       Pf[i][j] = s;
     }
+  }
 }
 
 
