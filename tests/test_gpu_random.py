@@ -1,0 +1,105 @@
+"""Randomised parity sweep (seeded): the HIP library through the C ABI vs the C restatement of the
+reference filter (oracle/yfm_oracle.c: dense N×N getrf+getri + logdet LU per step) over random
+shapes and inputs — every model kind, maturity counts from 1 (fewer than the state dimension:
+the capacitance path) to 96 (the lane-group kernel), short and long panels, NaN columns
+(leading, interior, all-NaN), ragged T_use windows, unconstrained and constrained θ.
+
+Rule (tests/test_gpu_parity.py): within 1e-9 of the oracle, relative to the loglik's term scale
+(max(|ll|, ½·nterms·N·log 2π): short random panels can sum to ≈ 0); where the oracle's own FP64
+arithmetic is further than that from exact arithmetic, the 40-digit restatement
+(oracle/kalman_mp.py) adjudicates: the kernel must be within 1e-10 of it, or at least as close
+to it as the oracle (TVλ EKF runs: within 10× the oracle's own distance).  −Inf / NaN patterns
+must match exactly."""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from oracle import kalman_ld as LD
+from oracle import kalman_mp as MP
+from yfm_amd import KIND_DNS, KIND_GNS, KIND_TVL
+from yfm_amd import synthetic as S
+from yfm_amd.params import n_params, transform_params
+
+pytestmark = pytest.mark.gpu
+
+D = ctypes.POINTER(ctypes.c_double)
+
+
+def c_oracle(kind, space, Y, mats, Th, T_use):
+    lib = ctypes.CDLL(str(ROOT / "oracle" / "libyfm_oracle.so"))
+    Yf = np.asfortranarray(Y)
+    Thf = np.asfortranarray(Th)
+    N, T = Yf.shape
+    P, B = Thf.shape
+    out = np.empty(B)
+    tu = None if T_use is None else np.ascontiguousarray(T_use, dtype=np.int32)
+    lib.yfm_oracle_loglik(kind, space, Yf.ctypes.data_as(D), N, T, np.ascontiguousarray(mats).ctypes.data_as(D),
+                          Thf.ctypes.data_as(D), P, B, None if tu is None else tu.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+                          out.ctypes.data_as(D), 8)
+    return out
+
+
+def random_case(rng, kind):
+    N = int(rng.choice([1, 2, 3, 7, 12, 30, 33, 64, 65, 96]))
+    if kind == KIND_TVL:
+        N = max(N, 1)
+    T = int(rng.choice([1, 2, 3, 5, 17, 40, 90]))
+    mats = np.sort(rng.choice(np.arange(1, 361), size=N, replace=False)).astype(np.float64)
+    Y = S.simulate_panel(kind, T, maturities=mats, seed=int(rng.integers(1 << 30))).copy(order="F")
+    pattern = rng.integers(4)
+    if pattern == 1 and T > 3:
+        Y[:, rng.choice(T, size=max(1, T // 8), replace=False)] = np.nan
+    elif pattern == 2 and T > 1:
+        Y[int(rng.integers(N)), 0] = np.nan  # leading partial-NaN column
+    B = 24
+    scale = 0.02 if kind == KIND_TVL else float(rng.choice([0.03, 0.1]))
+    Th = S.theta_batch(kind, B, seed=int(rng.integers(1 << 30)), bad_frac=0.1 if kind != KIND_TVL else 0.0,
+                       scale=scale)
+    space = int(rng.integers(2))
+    if space == 1:
+        Th = transform_params(kind, Th)
+    T_use = None
+    if rng.integers(2) and T > 1:
+        T_use = rng.integers(1, T + 1, size=B).astype(np.int32)
+    return N, T, mats, Y, Th, space, T_use
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_cases_vs_c_oracle(engine, seed):
+    rng = np.random.default_rng(1000 + seed)
+    kind = [KIND_DNS, KIND_GNS, KIND_TVL][seed % 3]
+    N, T, mats, Y, Th, space, T_use = random_case(rng, kind)
+    assert Th.shape[0] == n_params(kind)
+    engine.set_panel(Y, mats)
+    got = engine.loglik(kind, Th, space=space, T_use=T_use)
+    ref = c_oracle(kind, space, Y, mats, Th, T_use)
+    what = dict(kind=kind, N=N, T=T, space=space, windows=T_use is not None)
+    assert np.array_equal(np.isnan(got), np.isnan(ref)), what
+    assert np.array_equal(np.isneginf(got), np.isneginf(ref)), (what, got, ref)
+    assert not np.isposinf(got).any()
+    fin = np.isfinite(ref)
+    # error scale: the loglik is a sum of per-step terms −½(log det F + v'F⁻¹v + N log 2π); FP64
+    # accuracy is relative to the terms' magnitude, not to a sum that may cancel to ≈ 0 (random
+    # short panels do that): scale = max(|ll|, ½·nterms·N·log 2π)
+    nobs = np.full(Th.shape[1], T) if T_use is None else T_use
+    scale = np.maximum(np.abs(ref), 0.5 * np.maximum(nobs - 2, 0) * N * np.log(2 * np.pi))
+    err = np.zeros_like(ref)
+    err[fin] = np.abs(got[fin] - ref[fin]) / np.maximum(scale[fin], 1e-300)
+    assert np.all((ref[fin] != 0.0) | (got[fin] == 0.0)), what  # loglik exactly 0 (T_use ≤ 2) is exact
+    for b in np.flatnonzero(fin & (err > 1e-9)):
+        tu = None if T_use is None else int(T_use[b])
+        Yw = Y if tu is None else Y[:, :tu]
+        if kind == KIND_TVL:
+            truth = float(LD.loglik_ld_tvl(mats, Yw, Th[:, b:b + 1], space)[0])
+        elif N > 40 and not np.isnan(Yw).any():
+            truth = float(LD.loglik_ld(kind, mats, Yw, Th[:, b:b + 1], space)[0])
+        else:  # 40-digit dense restatement (affordable at small N)
+            truth = MP.loglik_mp(kind, mats, Y, Th[:, b], space, T_use=tu)[0]
+        e_gt = abs(got[b] - truth) / max(abs(truth), scale[b])
+        e_or = abs(ref[b] - truth) / max(abs(truth), scale[b])
+        factor = 10.0 if kind == KIND_TVL else 1.0
+        assert e_gt <= max(1e-10, factor * e_or), (what, b, err[b], e_gt, e_or)

@@ -79,6 +79,7 @@ struct yfm_ctx {
   DevBuf flags;  // 2 × unsigned int
   DevBuf scratch;  // per-candidate work records (TVλ init)
   DevBuf traj, init_bad;       // trajectory-mode state records, per-candidate init-throw marks
+  DevBuf defer;                // [count, list...] of candidates handed from the per-lane to the group kernel
   DevBuf tiled_raw, tiled_panel;  // get_loss_array with K > 1 passes: the panel tiled K times
   // TVλ maturity-jump tables, one per lane count L = 2^l (built lazily, reset by set_panel)
   std::vector<double> mats_host;
@@ -209,8 +210,18 @@ int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int 
     if (int r = tvl_gaps(ctx, lanes, g)) return r;
     e = yfm::launch_tvl(a, g, lanes);
   } else {
-    // N ≤ 64: one filter per lane (MFMA Z'y); larger N: one filter per lane group
-    e = yfm::fixedz_np_for(ctx->N) > 0 ? yfm::launch_fixedz(kind, a) : yfm::launch_fixedz_group(kind, a);
+    // N ≤ 64: one filter per lane (MFMA Z'y), then the lane-group kernel for the candidates it
+    // deferred (ill-conditioned Z'Z); larger N: one filter per lane group for every candidate
+    if (yfm::fixedz_np_for(ctx->N) > 0) {
+      YFM_HIP_CHECK(ctx->defer.ensure(sizeof(int) * ((size_t)B + 1)));
+      a.defer_count = static_cast<int*>(ctx->defer.p);
+      a.defer_list = a.defer_count + 1;
+      YFM_HIP_CHECK(hipMemsetAsync(a.defer_count, 0, sizeof(int), s));
+      e = yfm::launch_fixedz(kind, a);
+      if (e == hipSuccess) e = yfm::launch_fixedz_group(kind, a);
+    } else {
+      e = yfm::launch_fixedz_group(kind, a);
+    }
   }
   if (e != hipSuccess) return set_error(YFM_EHIP, "kernel launch: %s", hipGetErrorString(e));
   return YFM_OK;
@@ -329,7 +340,7 @@ void yfm_destroy(yfm_ctx* ctx) {
   for (DevBuf* b : {&ctx->panel, &ctx->mats, &ctx->raw, &ctx->theta, &ctx->out, &ctx->tuse, &ctx->rec_beta,
                     &ctx->rec_P, &ctx->flags, &ctx->scratch})
     b->release();
-  for (DevBuf* b : {&ctx->traj, &ctx->init_bad, &ctx->tiled_raw, &ctx->tiled_panel}) b->release();
+  for (DevBuf* b : {&ctx->traj, &ctx->init_bad, &ctx->tiled_raw, &ctx->tiled_panel, &ctx->defer}) b->release();
   for (DevBuf& b : ctx->gap_buf) b.release();
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;

@@ -201,7 +201,9 @@ __device__ __forceinline__ bool init_state(const Params<M, LEAD>& p, double (&be
 //   W = B̃⁻¹ P = P B⁻¹ (symmetric),  K v = W Z'v,  P_{t|t} = σ² W,
 //   v'F⁻¹v = (v'v − u'Wu)/σ²,  det F = σ^{2(N−M)} det B̃.
 // Outputs the upper triangle of W and det B̃ (its sign is the sign of det F).
-template <int M>
+// SYM: return the symmetric part of the computed W (used by the fixed-loading models, whose
+// capacitance lanes are exactly those with near-singular Z'Z); otherwise its upper triangle.
+template <int M, bool SYM = false>
 struct Capacitance {
   __device__ __forceinline__ static void solve(const double (&P)[M][M], const double (&G)[M][M], double sigma2,
                                                double (&W)[M][M], double& det) {
@@ -271,10 +273,13 @@ struct Capacitance {
         X[k][c] = s * r;
       }
     }
+    // W = B̃⁻¹P is symmetric in exact arithmetic; the computed one is not (its asymmetry grows
+    // with B̃'s conditioning — measured 7e-9 on the loglik from using one triangle when Z'Z is
+    // near-singular).  Use the symmetric part.
 #pragma unroll
     for (int i = 0; i < M; ++i)
 #pragma unroll
-      for (int j = i; j < M; ++j) W[i][j] = X[i][j];
+      for (int j = i; j < M; ++j) W[i][j] = SYM ? 0.5 * (X[i][j] + X[j][i]) : X[i][j];
     det = sgn * prod;
   }
 };

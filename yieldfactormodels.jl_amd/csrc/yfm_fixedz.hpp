@@ -75,7 +75,10 @@ __device__ __forceinline__ void collapsed_update(const double (&zt)[M - 1], doub
 }
 
 
-template <int M, int LEAD, bool RECORD>
+// CAP: whether this filter runs the capacitance form itself.  The one-filter-per-lane kernel
+// (CAP = false) defers lanes whose Z'Z is ill-conditioned to the lane-group kernel, which has
+// the per-maturity data the capacitance form's innovation needs (CAP = true).
+template <int M, int LEAD, bool RECORD, bool CAP>
 struct FixedZFilter {
   Params<M, LEAD> p;
   double sigma2, rsig2;
@@ -110,8 +113,24 @@ struct FixedZFilter {
 #pragma unroll
     for (int i = 0; i < M; ++i) detG *= A[i][i];
     detG = fabs(detG);
-    // Z'Z must be numerically nonsingular: det / ∏ diag (Hadamard ratio, ≤ 1).
-    collapsed = ok && (N >= M) && (detG > 1e-13 * hadamard);
+    // The collapsed form's rounding grows with κ(Z'Z) (measured: ≈ κ·3e-18 relative on the
+    // loglik); κ₁ = ‖G‖₁‖G⁻¹‖₁ is ≈ 400 for DNS and ≤ 3e5 for GNS5 on the usual maturity grids,
+    // ~1e15 when the loadings are collinear (e.g. three long maturities).  Above 1e8 the lane
+    // takes the capacitance form, which does not invert Z'Z.
+    double nG = 0.0, nX = 0.0;
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      double cg = 0.0, cx = 0.0;
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        cg += fabs(G[i][j]);
+        cx += fabs(X[i][j]);
+      }
+      nG = fmax(nG, cg);
+      nX = fmax(nX, cx);
+    }
+    (void)hadamard;
+    collapsed = ok && (N >= M) && (nG * nX < 1e8);
     logdetG = collapsed ? log(detG) : 0.0;
 #pragma unroll
     for (int i = 0; i < M; ++i)
@@ -122,8 +141,12 @@ struct FixedZFilter {
 
   // One filter! call on column t given z̃_t (zc), (ȳ, ỹ'ỹ) = yb and (nan flag, y'y) = meta.
   // `fast`: the caller guarantees t ≥ 1, a data column, an active collapsed lane (no masking).
+  // `resid(beta, u, vv)`: u = Z'v and v'v of the innovation v = y_t − Zβ formed per maturity,
+  // as the reference does (filter.jl:143-144) — used on capacitance lanes (Z'Z near-singular),
+  // where reconstructing v'v from y'y, Z'y and Z'Z would lose ‖Z‖‖β‖/‖v‖ digits.
+  template <class Resid>
   __device__ __forceinline__ void step(int t, const double (&zc)[M - 1], double2 yb_c, double2 meta_c, bool fast,
-                                       int my_steps, int my_data) {
+                                       int my_steps, int my_data, Resid&& resid) {
     if (fast) {
       double bf[M], Pf[M][M], det, q;
       collapsed_update<M>(zc, yb_c.x, yb_c.y, R, rsig2, beta, Pm, bf, Pf, det, q);
@@ -161,28 +184,14 @@ struct FixedZFilter {
     double det, q;
     double bf[M];
     double Pf[M][M];
-    if (collapsed) {
+    if (!CAP || collapsed) {
       collapsed_update<M>(zc, yb_c.x, yb_c.y, R, rsig2, beta, Pm, bf, Pf, det, q);
-    } else {
-      // capacitance form on uncentered sums: Z'y = (Nȳ, z̃ + ȳ G[1:,0]), y'y
-      double zy[M];
-      zy[0] = (double)N * yb_c.x;
-#pragma unroll
-      for (int j = 1; j < M; ++j) zy[j] = fma(yb_c.x, R[j][0], zc[j - 1]);
-      double u[M];
-      double bgb = 0.0, bzy = 0.0;
-#pragma unroll
-      for (int i = 0; i < M; ++i) {
-        double g = 0.0;
-#pragma unroll
-        for (int j = 0; j < M; ++j) g = fma(R[i][j], beta[j], g);
-        u[i] = zy[i] - g;
-        bgb = fma(beta[i], g, bgb);
-        bzy = fma(beta[i], zy[i], bzy);
-      }
-      const double vv = fma(-2.0, bzy, meta_c.y) + bgb;
+    } else if constexpr (CAP) {
+      // capacitance form (R holds G = Z'Z on these lanes)
+      double u[M], vv;
+      resid(beta, u, vv);
       double W[M][M];
-      Capacitance<M>::solve(Pm, R, sigma2, W, det);
+      Capacitance<M, true>::solve(Pm, R, sigma2, W, det);
 #pragma unroll
       for (int i = 0; i < M; ++i)
 #pragma unroll

@@ -35,7 +35,7 @@ __global__ __launch_bounds__(kGBlock, 2) void fixedz_group_kernel(
     const double* __restrict__ theta, int P, int B, int space, const double* __restrict__ panel, int ldp, int np,
     int T, int N, int TC, const double* __restrict__ mats, const int* __restrict__ T_use, double* __restrict__ out,
     unsigned int* __restrict__ flags, double* __restrict__ rec_beta, double* __restrict__ rec_P, int horizon,
-    int rec_len) {
+    int rec_len, const int* __restrict__ defer_list, const int* __restrict__ defer_count) {
   constexpr int NZ = M - 1;
   constexpr int GPB = kGBlock / L;  // filters per block
   constexpr int MPL = group_max_per_lane<M>();
@@ -46,9 +46,17 @@ __global__ __launch_bounds__(kGBlock, 2) void fixedz_group_kernel(
 
   const int tid = threadIdx.x;
   const int j = tid % L;
-  const int b = blockIdx.x * GPB + tid / L;
-  const bool live = b < B;
-  const int bb = live ? b : (B - 1);
+  // deferred mode: filter g evaluates candidate defer_list[g] (ill-conditioned Z'Z lanes of
+  // the per-lane kernel), g < *defer_count; blocks past the list exit before any barrier
+  const int g = blockIdx.x * GPB + tid / L;
+  int nd = B;
+  if (defer_list) {
+    nd = *defer_count;
+    if ((int)blockIdx.x * GPB >= nd) return;
+  }
+  const bool live = g < nd;
+  const int b = defer_list ? (live ? defer_list[g] : 0) : g;
+  const int bb = live ? b : (defer_list ? defer_list[0] : B - 1);
   const int nobs = T_use ? T_use[bb] : T;
   const int my_steps = horizon > 0 ? nobs + horizon : nobs - 1;  // as yfm_kernels.hip
   const int my_data = horizon > 0 ? nobs : nobs - 1;
@@ -57,7 +65,7 @@ __global__ __launch_bounds__(kGBlock, 2) void fixedz_group_kernel(
   __syncthreads();
   atomicMax(&s_nobs_max, live ? my_steps : 0);
 
-  FixedZFilter<M, LEAD, RECORD> f;
+  FixedZFilter<M, LEAD, RECORD, true> f;
   decode_params<M, LEAD>(theta + (size_t)bb * P, space, f.p);
 
   // this lane's loadings (dns.jl:51-65; the GNS5 extension adds a second (S, C) pair)
@@ -149,7 +157,32 @@ __global__ __launch_bounds__(kGBlock, 2) void fixedz_group_kernel(
     for (int c = 0; c < NZ; ++c) zc[c] = group_sum<L>(zc[c]);
     const double2 yb = *reinterpret_cast<const double2*>(col + np);
     const double2 meta = *reinterpret_cast<const double2*>(col + np + 2);
-    f.step(t, zc, yb, meta, false, my_steps, my_data);
+    // capacitance lanes (near-singular Z'Z): the innovation per owned maturity, group-reduced
+    auto resid = [&](const double (&bt)[M], double (&u)[M], double& vv) {
+      double acc[M + 1];
+#pragma unroll
+      for (int c = 0; c <= M; ++c) acc[c] = 0.0;
+#pragma unroll
+      for (int k = 0; k < MPL; ++k) {
+        const int i = j + k * L;
+        if (i < N) {
+          double yh = bt[0];
+#pragma unroll
+          for (int c = 0; c < NZ; ++c) yh = fma(Zl[k][c], bt[c + 1], yh);
+          const double v = (col[i] + yb.x) - yh;
+          acc[0] += v;
+#pragma unroll
+          for (int c = 0; c < NZ; ++c) acc[c + 1] = fma(Zl[k][c], v, acc[c + 1]);
+          acc[M] = fma(v, v, acc[M]);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c <= M; ++c) acc[c] = group_sum<L>(acc[c]);
+#pragma unroll
+      for (int c = 0; c < M; ++c) u[c] = acc[c];
+      vv = acc[M];
+    };
+    f.step(t, zc, yb, meta, false, my_steps, my_data, resid);
     if constexpr (RECORD) {
       if (live && j == 0) f.record(t, b, my_steps, rec_len, rec_beta, rec_P);
     }
@@ -175,11 +208,11 @@ hipError_t launch_group_l(const LaunchArgs& a, int TC) {
   if (a.rec_beta) {
     hipLaunchKernelGGL((fixedz_group_kernel<L, M, LEAD, true>), dim3(grid), dim3(kGBlock), shmem, a.stream, a.theta,
                        a.P, a.B, a.space, a.panel, a.ldp, a.np, a.T, a.N, TC, a.mats, a.T_use, a.out, a.flags,
-                       a.rec_beta, a.rec_P, a.horizon, a.rec_len);
+                       a.rec_beta, a.rec_P, a.horizon, a.rec_len, a.defer_list, a.defer_count);
   } else {
     hipLaunchKernelGGL((fixedz_group_kernel<L, M, LEAD, false>), dim3(grid), dim3(kGBlock), shmem, a.stream, a.theta,
                        a.P, a.B, a.space, a.panel, a.ldp, a.np, a.T, a.N, TC, a.mats, a.T_use, a.out, a.flags,
-                       nullptr, nullptr, 0, 0);
+                       nullptr, nullptr, 0, 0, a.defer_list, a.defer_count);
   }
   return hipGetLastError();
 }
@@ -208,6 +241,7 @@ int group_lanes_for(int kind, int N) {
 }
 
 hipError_t launch_fixedz_group(int kind, const LaunchArgs& a) {
+  // a.defer_list != nullptr: evaluate only the candidates the per-lane kernel deferred
   const int L = group_lanes_for(kind, a.N);
   if (L < 0) return hipErrorInvalidValue;
   int TC = (kGPre * kGBlock) / a.ldp;  // columns per chunk: the prefetch registers hold ≤ kGPre·256

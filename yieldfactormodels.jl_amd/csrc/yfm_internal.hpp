@@ -19,6 +19,8 @@ struct LaunchArgs {
   double* scratch;      // per-candidate work records (tvl_scratch_bytes)
   int horizon = 0;      // 0: loglik mode; ≥ 1: trajectory mode (predict / forecast / loss array)
   int rec_len = 0;      // recorded steps per candidate (the last rec_len), stride of rec_beta / rec_P
+  int* defer_list = nullptr;   // per-lane fixed-loading kernel → lane-group kernel hand-off (B ints)
+  int* defer_count = nullptr;  // 1 int, zeroed before the per-lane kernel
   hipStream_t stream;
 };
 

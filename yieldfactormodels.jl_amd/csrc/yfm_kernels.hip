@@ -107,7 +107,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     const double* __restrict__ theta, int P, int B, int space, const double* __restrict__ panel, int T, int N,
     const double* __restrict__ mats, const int* __restrict__ T_use, double* __restrict__ out,
     unsigned int* __restrict__ flags, double* __restrict__ rec_beta, double* __restrict__ rec_P, int horizon,
-    int rec_len) {
+    int rec_len, int* __restrict__ defer_list, int* __restrict__ defer_count) {
   constexpr int LDP = NP + 4;
   constexpr int CH = kTC * LDP;               // doubles per chunk
   constexpr int PER = (CH + kBlock - 1) / kBlock;
@@ -213,16 +213,20 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     }
   }
 
-  FixedZFilter<M, LEAD, RECORD> f;
+  FixedZFilter<M, LEAD, RECORD, false> f;
   f.p = p;
   f.setup(G, N);
+  // ill-conditioned Z'Z: this candidate is evaluated by the lane-group kernel instead (capacitance
+  // form with the innovation formed per maturity); its lane here runs along without writing
+  const bool defer = live && !f.collapsed;
+  if (defer) defer_list[atomicAdd(defer_count, 1)] = b;
 
   // wave-uniform facts for the fast path
   int wmin = live ? my_data : 0x7fffffff;
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) wmin = min(wmin, __shfl_xor(wmin, off));
   const int wave_min_data = __builtin_amdgcn_readfirstlane(wmin);
-  const bool wave_all_collapsed = __ballot(!f.collapsed) == 0ull;
+  const bool wave_all_collapsed = true;  // non-collapsed lanes are deferred (their values are discarded)
 
   __syncthreads();
   const int nsteps = max(s_nobs_max, 0);
@@ -259,11 +263,11 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   // one filter step given z̃_t (zc), (ȳ, ỹ'ỹ) and (nanflag, y'y) of column t
   auto do_step = [&](int t, const double (&zc)[NZ], double2 yb_c, double2 meta_c) {
     const bool fast = (t >= 1) && (meta_c.x == 0.0) && (t < wave_min_data) && wave_all_collapsed;
-    f.step(t, zc, yb_c, meta_c, fast, my_steps, my_data);
+    f.step(t, zc, yb_c, meta_c, fast, my_steps, my_data, [](const double (&)[M], double (&)[M], double&) {});
   };
   auto record = [&](int t) {
     if constexpr (RECORD) {
-      if (live) f.record(t, b, my_steps, rec_len, rec_beta, rec_P);
+      if (live && !defer) f.record(t, b, my_steps, rec_len, rec_beta, rec_P);
     }
   };
   auto rotate = [&](int t) {  // after step t: if chunk c = t / kTC is done, its buffer takes chunk c + 2
@@ -364,7 +368,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     }
   }
 
-  if (!live) return;
+  if (!live || defer) return;
   const double ll = f.loglik(nobs, flags);
   out[b] = ll;
 }
@@ -384,10 +388,11 @@ static hipError_t launch_fixedz_np(const LaunchArgs& a) {
   if (a.rec_beta) {
     hipLaunchKernelGGL((fixedz_loglik_kernel<NP, M, LEAD, true>), dim3(grid), dim3(kBlock), 0, a.stream, a.theta, a.P,
                        a.B, a.space, a.panel, a.T, a.N, a.mats, a.T_use, a.out, a.flags, a.rec_beta, a.rec_P,
-                       a.horizon, a.rec_len);
+                       a.horizon, a.rec_len, a.defer_list, a.defer_count);
   } else {
     hipLaunchKernelGGL((fixedz_loglik_kernel<NP, M, LEAD, false>), dim3(grid), dim3(kBlock), 0, a.stream, a.theta,
-                       a.P, a.B, a.space, a.panel, a.T, a.N, a.mats, a.T_use, a.out, a.flags, nullptr, nullptr, 0, 0);
+                       a.P, a.B, a.space, a.panel, a.T, a.N, a.mats, a.T_use, a.out, a.flags, nullptr, nullptr, 0, 0,
+                       a.defer_list, a.defer_count);
   }
   return hipGetLastError();
 }

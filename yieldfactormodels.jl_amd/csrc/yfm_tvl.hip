@@ -40,10 +40,11 @@ constexpr int kTvlPre = 8;  // panel doubles prefetched per thread per chunk (â‰
 }  // namespace
 
 // Sufficient statistics of one EKF step, indices into the accumulator array.
-// Î£ Z_c (c = 2..4), the Gram entries, and Î£ Z_c y (c = 2..4); Î£ y and y'y come from the
-// prepared panel, so the innovation v = y âˆ’ Z[:,1:3]Î²[1:3] is never formed per maturity:
-// u = Z'v = Z'y âˆ’ G[:,1:3]Î²[1:3] and v'v = y'y âˆ’ 2Î²'Z'y + Î²'GÎ² after the reduction.
-enum : int { S2 = 0, S3, S4, G22, G23, G24, G33, G34, G44, Y2, Y3, Y4, NSTAT };
+// Î£ Z_c (c = 2..4), the Gram entries, u = Z'v and v'v, with the innovation
+// v = y âˆ’ Z[:,1:3]Î²[1:3] formed per maturity as the reference does (filter.jl:33-34): the
+// uncentered reconstruction v'v = y'y âˆ’ 2Î²'Z'y + Î²'GÎ² loses â€–Zâ€–â€–Î²â€–/â€–vâ€– digits when the
+// loadings are nearly collinear (measured: 1.8e-8 on a random N = 33, T = 3 case).
+enum : int { S2 = 0, S3, S4, G22, G23, G24, G33, G34, G44, U1, U2, U3, U4, VV, NSTAT };
 
 // Per-candidate record written by tvl_init_kernel: the decoded parameters and the
 // initial state, so the filter kernel never holds the 10Ã—10 Lyapunov system in VGPRs.
@@ -91,8 +92,8 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
   constexpr int GPB = kTvlBlock / L;  // filters per block
   extern __shared__ __attribute__((aligned(16))) double smem[];
   double2* s_mr = reinterpret_cast<double2*>(smem);  // (m_i, 1/m_i)
-  double* s_meta = smem + 2 * N;                      // per staged column: (NaN flag, È³, y'y)
-  double* s_y = s_meta + 3 * TC;                      // TC columns of N yields (column-major, stride N)
+  double* s_nan = smem + 2 * N;                       // TC NaN flags of the staged chunk
+  double* s_y = s_nan + TC;                           // TC columns of N yields (column-major, stride N)
   double* s_w = s_y + TC * N;                         // per group: e^{-Î» d_k}, k < K (â‰¤ kTvlGaps)
   int* s_gi = reinterpret_cast<int*>(s_w + GPB * kTvlGaps);  // gap index of the jump i â†’ i + L
   __shared__ double s_gd[kTvlGaps];
@@ -155,7 +156,7 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
 
   // ---- panel staging: chunk c (columns cTC .. cTC+TC-1) in LDS, chunk c+1 in registers ----
   double pre[kTvlPre];
-  double pre_meta = 0.0;
+  double pre_nan = 0.0;
   auto load_chunk = [&](int c) {
     const size_t base = (size_t)c * CHY;
     const size_t lim = (size_t)T * N;
@@ -165,9 +166,8 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
       const size_t g = base + e;
       pre[r] = (e < CHY && g < lim) ? Y[g] : 0.0;
     }
-    const int tc = c * TC + tid / 3;  // thread 3k + w loads (NaN flag, È³, y'y)[w] of column k
-    const int off = (tid % 3 == 0) ? np + 2 : (tid % 3 == 1) ? np : np + 3;
-    pre_meta = (tid < 3 * TC && tc < T) ? prep[(size_t)tc * ldp + off] : 0.0;
+    const int tc = c * TC + tid;
+    pre_nan = (tid < TC && tc < T) ? prep[(size_t)tc * ldp + np + 2] : 0.0;
   };
   auto store_chunk = [&]() {
 #pragma unroll
@@ -175,7 +175,7 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
       const int e = r * kTvlBlock + tid;
       if (e < CHY) s_y[e] = pre[r];
     }
-    if (tid < 3 * TC) s_meta[tid] = pre_meta;
+    if (tid < TC) s_nan[tid] = pre_nan;
   };
   if (nsteps > 0) {
     load_chunk(0);
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
     const int tt = t % TC;
     const bool act = t < my_steps;
     const bool acc = t >= 1;  // Julia t > 1 (filter.jl:194)
-    const bool nan_col = s_meta[3 * tt] != 0.0 || t >= my_data;
+    const bool nan_col = s_nan[tt] != 0.0 || t >= my_data;
     if (act && nan_col) {
       // filter.jl:13-29: prediction only; F, Fâ»Â¹, v stale â†’ the loglik re-adds the last term
       double bf[M], Pf[M][M];
@@ -234,9 +234,12 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
         s[G33] = fma(z3, z3, s[G33]);
         s[G34] = fma(z3, z4, s[G34]);
         s[G44] = fma(z4, z4, s[G44]);
-        s[Y2] = fma(z2, y, s[Y2]);
-        s[Y3] = fma(z3, y, s[Y3]);
-        s[Y4] = fma(z4, y, s[Y4]);
+        const double v = y - fma(beta[2], z3, fma(beta[1], z2, beta[0]));  // y âˆ’ Z[:,1:3]Î²[1:3]
+        s[U1] += v;
+        s[U2] = fma(z2, v, s[U2]);
+        s[U3] = fma(z3, v, s[U3]);
+        s[U4] = fma(z4, v, s[U4]);
+        s[VV] = fma(v, v, s[VV]);
       };
       if (K > 0) {
         // few distinct jumps d_k = m_{i+L} âˆ’ m_i: z_{i+L} = z_i Â· e^{-Î» d_k}, one exp per lane
@@ -275,18 +278,8 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
       G[2][2] = s[G33];
       G[2][3] = G[3][2] = s[G34];
       G[3][3] = s[G44];
-      // u = Z'y âˆ’ G[:,1:3]Î²[1:3],  v'v = y'y âˆ’ 2Î²[1:3]'(Z'y)[1:3] + Î²[1:3]'G[1:3,1:3]Î²[1:3]
-      const double zy[M] = {(double)N * s_meta[3 * tt + 1], s[Y2], s[Y3], s[Y4]};
-      double u[M];
-      double vv = s_meta[3 * tt + 2];
-#pragma unroll
-      for (int c = 0; c < M; ++c) {
-        double g = 0.0;
-#pragma unroll
-        for (int d = 0; d < 3; ++d) g = fma(G[c][d], beta[d], g);
-        u[c] = zy[c] - g;
-        if (c < 3) vv = fma(beta[c], g - 2.0 * zy[c], vv);
-      }
+      const double u[M] = {s[U1], s[U2], s[U3], s[U4]};
+      const double vv = s[VV];
 
       double W[M][M], det;
       Capacitance<M>::solve(Pm, G, sigma2, W, det);
@@ -367,7 +360,7 @@ template <int L>
 hipError_t launch_tvl_l(const LaunchArgs& a, const TvlGaps& g, int TC) {
   constexpr int GPB = kTvlBlock / L;
   const int grid = (a.B + GPB - 1) / GPB;
-  const size_t shmem = sizeof(double) * (size_t)(2 * a.N + 3 * TC + TC * a.N + GPB * kTvlGaps) + sizeof(int) * a.N;
+  const size_t shmem = sizeof(double) * (size_t)(2 * a.N + TC + TC * a.N + GPB * kTvlGaps) + sizeof(int) * a.N;
   hipLaunchKernelGGL(tvl_init_kernel, dim3((a.B + 255) / 256), dim3(256), 0, a.stream, a.theta, a.P, a.B, a.space,
                      a.scratch);
   if (a.rec_beta) {
