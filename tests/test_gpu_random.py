@@ -103,3 +103,57 @@ def test_random_cases_vs_c_oracle(engine, seed):
         e_or = abs(ref[b] - truth) / max(abs(truth), scale[b])
         factor = 10.0 if kind == KIND_TVL else 1.0
         assert e_gt <= max(1e-10, factor * e_or), (what, b, err[b], e_gt, e_or)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_trajectories_vs_oracle(engine, seed):
+    """predict (NaN-padded horizon, ragged windows) and get_loss_array on random shapes vs the NumPy
+    oracle (filter.jl:211-282): normwise 1e-9 per output array; NaN / −Inf patterns exact."""
+    from oracle import kalman_oracle as O
+    from yfm_amd.params import state_dim
+    rng = np.random.default_rng(2000 + seed)
+    kind = [KIND_DNS, KIND_GNS, KIND_TVL][seed % 3]
+    N = int(rng.choice([1, 3, 7, 30, 65]))
+    T = int(rng.choice([2, 5, 17, 40]))
+    mats = np.sort(rng.choice(np.arange(1, 361), size=N, replace=False)).astype(np.float64)
+    Y = S.simulate_panel(kind, T, maturities=mats, seed=int(rng.integers(1 << 30))).copy(order="F")
+    if T > 4 and rng.integers(2):
+        Y[:, int(rng.integers(1, T))] = np.nan
+    B = 5
+    Th = transform_params(kind, S.theta_batch(kind, B, seed=int(rng.integers(1 << 30)), bad_frac=0.0,
+                                              scale=0.02 if kind == KIND_TVL else 0.05))
+    h = int(rng.integers(1, 5))
+    tu = rng.integers(1, T + 1, size=B).astype(np.int32)
+    engine.set_panel(Y, mats)
+    r = engine.predict(kind, Th, space=1, T_use=tu, horizon=h)
+    la = engine.loss_array(kind, Th, space=1, T_use=tu)
+    for b in range(B):
+        s = O.KalmanState.fresh(kind, mats, state_dim(kind))
+        O.set_params(s, Th[:, b])
+        ref = O.predict(s, O.pad_nan(Y[:, :tu[b]], h))
+        n = tu[b] + h - 1
+        if kind == KIND_TVL:  # EKF: the FP64 noise-floor rule of tests/test_gpu_predict.py
+            from test_gpu_predict import assert_close_floor
+            A_ld = LD.predict_traj_tvl(mats, Y[:, :tu[b]], Th[:, b:b + 1], horizon=h)[0, :n + 1]
+            A_64 = LD.predict_traj_tvl(mats, Y[:, :tu[b]], Th[:, b:b + 1], horizon=h, dtype=np.float64)[0, :n + 1]
+            tru = {"factors": A_ld[1:].T, "preds": LD.fitted_tvl(mats, A_ld[:n]).T}
+            alt = {"factors": A_64[1:].T, "preds": LD.fitted_tvl(mats, A_64[:n]).T}
+            for k in ("factors", "preds"):
+                assert_close_floor(r[k][:, :n, b], ref[k], tru[k], alt[k], what=(seed, k, b))
+        for k, v in ref.items():
+            got = r[k][:, :n, b]
+            assert np.array_equal(np.isnan(got), np.isnan(v)), (seed, k, b)
+            fin = np.isfinite(v)
+            if fin.any() and kind != KIND_TVL:
+                sc = max(np.abs(v[fin]).max(), 1e-300)
+                assert np.abs(got[fin] - v[fin]).max() / sc <= 1e-9, (seed, k, b, N, T)
+            assert np.isnan(r[k][:, n:, b]).all()
+        s = O.KalmanState.fresh(kind, mats, state_dim(kind))
+        O.set_params(s, Th[:, b])
+        ref_la = O.get_loss_array(s, Y[:, :tu[b]])
+        got_la = la[:tu[b] - 1, b]
+        if np.isscalar(ref_la):
+            assert np.isneginf(got_la).all() or got_la.size == 0, (seed, b)
+        elif kind != KIND_TVL:
+            sc = max(np.abs(ref_la).max(), 1e-300) if ref_la.size else 1.0
+            assert np.abs(got_la - ref_la).max(initial=0.0) / sc <= 1e-9, (seed, b)
