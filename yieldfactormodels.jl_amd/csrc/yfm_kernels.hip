@@ -189,7 +189,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   // Gathered once through the wave's scratch, 16 candidates at a time.
   double Af[USE_MFMA ? NRT : 1][USE_MFMA ? NK : 1];
   if constexpr (USE_MFMA) {
-    constexpr int ZS = 4 * NK;  // padded maturity stride of the staging image
+    constexpr int ZS = 4 * NK + 1;  // maturity stride of the staging image (odd: conflict-free LDS)
     constexpr int QT = NRT / 4;  // row tiles per quarter (16 candidates)
     static_assert(16 * NZ * ZS <= SCR, "staging fits the scratch");
     double* st = scratch[wave];
