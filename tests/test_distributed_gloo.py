@@ -123,3 +123,64 @@ def test_bench_sharding_covers_every_unit_once(config):
                 seen += list(range(w.extra["offset"], w.extra["offset"] + w.Theta.shape[1]))
         assert len(seen) == len(set(seen)) == w.global_batch
         assert max(sizes) - min(sizes) <= (60 if config == 4 else 1)
+
+
+def test_balanced_window_assignment():
+    T_use = np.arange(361, 601)
+    for world in (1, 2, 4, 8):
+        parts = D.balanced_window_assignment(T_use, world)
+        allidx = np.sort(np.concatenate(parts))
+        np.testing.assert_array_equal(allidx, np.arange(len(T_use)))
+        loads = [T_use[p].sum() for p in parts]
+        assert max(loads) - min(loads) <= T_use.max()
+
+
+def _estimate_worker(rank, world, port, Theta0, T_use, Y, mats, ret):
+    """Each rank runs its chains on the CPU restatement (oracle/optim_nm.py over the NumPy oracle)
+    — the collective pattern is the one the GPU path uses."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import math
+    from oracle import kalman_oracle as O
+    from oracle import optim_nm as NM
+    from yfm_amd.params import transform_params, untransform_params
+
+    def estimate(Th, tu):
+        out = dict(theta_c=np.empty_like(Th), ll=np.empty(Th.shape[1]), status=np.zeros(Th.shape[1], np.int32))
+        for b in range(Th.shape[1]):
+            def f(th, b=b):
+                v = O.loglik(0, mats, 3, Y[:, :tu[b]], th)
+                if math.isnan(v):
+                    raise NM.InitThrow()
+                return -v
+            r = NM.estimate_steps(f, Th[:, b], transform=lambda x: transform_params(0, x),
+                                  untransform=lambda x: untransform_params(0, x), max_group_iters=1, iterations=6)
+            out["theta_c"][:, b], out["ll"][b], out["status"][b] = r.theta_c, r.ll, r.status
+        return out
+
+    res = D.sharded_estimate(Theta0, T_use, estimate)
+    if rank == 0:
+        ret["theta_c"] = res["theta_c"]
+        ret["ll"] = res["ll"]
+        single = estimate(Theta0, T_use)
+        ret["single_theta_c"] = single["theta_c"]
+        ret["single_ll"] = single["ll"]
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_estimate_equals_single_process():
+    """The distributed rolling re-estimation (yfm_amd.distributed.sharded_estimate) returns, on every
+    rank, exactly the per-window results a single process computes (chains are independent)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+    from yfm_amd import synthetic as S
+    Y = S.simulate_panel(0, 30)
+    mats = S.maturities_30()
+    T_use = np.array([30, 12, 25, 20, 8], dtype=np.int32)
+    Theta0 = np.repeat(S.theta0_constrained(0)[:, None], 5, axis=1)
+    mgr = mp.Manager()
+    ret = mgr.dict()
+    mp.spawn(_estimate_worker, args=(2, _free_port(), Theta0, T_use, Y, mats, ret), nprocs=2, join=True)
+    np.testing.assert_array_equal(ret["theta_c"], ret["single_theta_c"])
+    np.testing.assert_array_equal(ret["ll"], ret["single_ll"])

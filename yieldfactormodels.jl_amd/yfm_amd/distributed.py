@@ -108,3 +108,47 @@ def sharded_loglik(Theta: np.ndarray, evaluate: Callable[[np.ndarray], torch.Ten
     allv = gather_logliks(local, counts, group)
     bi, bv = best_candidate(local, lo, group)
     return GatherResult(allv, bi, bv)
+
+
+def balanced_window_assignment(T_use, world: int) -> list[np.ndarray]:
+    """Assign estimation chains (one per window, cost ∝ window length) to ranks: longest first onto
+    the least-loaded rank (LPT), so every rank gets about the same number of filter steps.  Returns
+    each rank's chain indices in ascending order (deterministic on every rank)."""
+    T_use = np.asarray(T_use, dtype=np.int64)
+    load = np.zeros(world)
+    parts = [[] for _ in range(world)]
+    for i in np.argsort(-T_use, kind="stable"):
+        r = int(np.argmin(load))
+        parts[r].append(int(i))
+        load[r] += T_use[i]
+    return [np.array(sorted(p), dtype=np.int64) for p in parts]
+
+
+def sharded_estimate(Theta0: np.ndarray, T_use, estimate: Callable, group=None, device=None) -> dict:
+    """Distributed batched estimate_steps!: the R chains (columns of Θ₀, windows T_use) are split
+    over the ranks by `balanced_window_assignment`; each rank runs `estimate(Θ₀_shard, T_use_shard)`
+    (a rank-local callable returning dict(theta_c P×r, ll r, status r), e.g. Engine.estimate on its
+    GPU) and the results are all-gathered into global chain order on every rank — the only
+    collective (RCCL with the nccl backend; no data-path exchange inside a chain)."""
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    T_use = np.asarray(T_use, dtype=np.int32)
+    P, R = Theta0.shape
+    parts = balanced_window_assignment(T_use, world)
+    mine = parts[rank]
+    if mine.size:
+        res = estimate(np.asfortranarray(Theta0[:, mine]), np.ascontiguousarray(T_use[mine]))
+        local = np.vstack([res["theta_c"], res["ll"][None, :], np.asarray(res["status"], np.float64)[None, :]])
+    else:
+        local = np.zeros((P + 2, 0))
+    m = max(len(p) for p in parts)
+    buf = torch.full((P + 2, m), float("nan"), dtype=torch.float64)
+    buf[:, :local.shape[1]] = torch.from_numpy(local)
+    if device is not None:
+        buf = buf.to(device)
+    out = torch.empty((world * (P + 2), m), dtype=torch.float64, device=buf.device)
+    dist.all_gather_into_tensor(out, buf.contiguous(), group=group)
+    out = out.view(world, P + 2, m).cpu().numpy()
+    glob = np.empty((P + 2, R))
+    for r, idx in enumerate(parts):
+        glob[:, idx] = out[r, :, :len(idx)]
+    return dict(theta_c=glob[:P], ll=glob[P], status=glob[P + 1].astype(np.int32), assignment=parts)

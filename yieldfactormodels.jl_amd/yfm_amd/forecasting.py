@@ -39,12 +39,22 @@ def _tails(r: dict, T_b: np.ndarray, h: int) -> dict:
     return out
 
 
-def _estimate_tasks(model, data, tasks, init_params, max_group_iters, group_tol, iterations):
+def _estimate_tasks(model, data, tasks, init_params, max_group_iters, group_tol, iterations, group=None):
     start = np.asarray(init_params, dtype=np.float64)
     start = start[:, 0] if start.ndim == 2 else start
     Theta0 = np.repeat(start[:, None], len(tasks), axis=1)
-    r = estimate_batch(model, data, Theta0, T_use=tasks, space=1, iterations=iterations,
-                       max_group_iters=max_group_iters, tol=group_tol)
+
+    def estimate(Th, tu):
+        return estimate_batch(model, data, Th, T_use=tu, space=1, iterations=iterations,
+                              max_group_iters=max_group_iters, tol=group_tol)
+
+    if group is not None:  # one process per GPU: windows split over the ranks, results all-gathered
+        import torch
+        from . import distributed as D
+        r = D.sharded_estimate(Theta0, tasks, estimate, group=group,
+                               device=torch.device("cuda", model.device) if torch.cuda.is_available() else None)
+    else:
+        r = estimate(Theta0, tasks)
     return r["theta_c"], r["ll"], r["status"]
 
 
@@ -164,10 +174,12 @@ def run_forecast_no_window(model, data, thread_id: str, in_sample_end: int, fore
 def run_rolling_forecasts(model, data, thread_id: str, in_sample_end: int, in_sample_start: int,
                           forecast_horizon: int, init_params, window_type: str = "both", max_group_iters: int = 10,
                           group_tol: float = 1e-8, reestimate: bool = True, params=None, iterations: int = 500,
-                          write_csv: bool = True) -> dict:
+                          write_csv: bool = True, group=None) -> dict:
     """forecasting.jl:16-51.  Returns {window_type: result dict}; writes the reference's CSVs when
     write_csv.  With window_type "both" the per-task estimation (identical for both window types,
-    both use the expanding sample) runs once and is shared."""
+    both use the expanding sample) runs once and is shared.  `group`: a torch.distributed process
+    group (one process per GPU) over which the per-task estimation chains are split (the
+    reference's multi-process task claiming, forecasting.jl:54-79, done as one sharded batch)."""
     if window_type in ("no_windowing", "simulation"):
         return {"expanding": run_forecast_no_window(model, data, thread_id, in_sample_end, forecast_horizon,
                                                     init_params, max_group_iters, group_tol, iterations, write_csv)}
@@ -178,7 +190,7 @@ def run_rolling_forecasts(model, data, thread_id: str, in_sample_end: int, in_sa
     tasks = np.arange(in_sample_end, data.shape[1] + 1, dtype=np.int32)
     est = None
     if reestimate:
-        est = _estimate_tasks(model, data, tasks, init_params, max_group_iters, group_tol, iterations)
+        est = _estimate_tasks(model, data, tasks, init_params, max_group_iters, group_tol, iterations, group)
     out = {}
     for wt in kinds:
         res = forecast_windows(model, data, in_sample_end, in_sample_start, forecast_horizon, wt, init_params,
