@@ -174,6 +174,17 @@ def cpu_baseline(w: Workload, seconds: float, gpu_out: np.ndarray):
             "parity": parity}
 
 
+def pmc_executed_flops(kernel_substr: str):
+    """Executed FP64 flops per eval of the dominant kernel from the committed PMC valu pass:
+    (FMA·2 + ADD + MUL)·64 + MFMA_MOPS_F64·512 (the expression of rocprof's SQ_INSTS_VALU_FLOPS_FP64)."""
+    for rnd in sorted((ROOT / "profiles").glob("r*/**/pmc_summary.json"), reverse=True):
+        d = json.loads(rnd.read_text())
+        for k, v in d.items():
+            if kernel_substr in k and "fp64_flops_executed_per_eval" in v:
+                return v["fp64_flops_executed_per_eval"]
+    return None
+
+
 def pmc_traffic(kernel_substr: str):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 --pmc passes
     (tools/profile_all.sh → profiles/<round>/**/pmc_summary.json), corrected as
@@ -294,6 +305,8 @@ def main():
                    else alg_flops(kind, N, M, T) * B)
     achieved = f_rank / (kernel_ms * 1e-3) / 1e12  # TFLOP/s of this GPU's launches
     traffic, traffic_src = pmc_traffic(DOMINANT[kind])
+    exe = pmc_executed_flops(DOMINANT[kind])
+    exe_tf = exe * B / (kernel_ms * 1e-3) / 1e12 if exe else None
     out_host = d_out.cpu().numpy()
     n_neginf, n_nan = int(np.isneginf(out_host).sum()), int(np.isnan(out_host).sum())
 
@@ -324,8 +337,11 @@ def main():
                          "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
                          "algorithmic_bytes": B * (P + 1) * 8 + T * (N + 4) * 8,
                          "kernel_ms": kernel_ms, "flops_per_eval": f_rank / max(B, 1),
-                         "note": "achieved = SURVEY §8d algorithmic flops of this GPU's batch ÷ HIP-event time of "
-                                 "its launches on the library stream"},
+                         "executed_tflops": exe_tf, "executed_frac": exe_tf / FP64_PEAK_TFLOPS if exe_tf else None,
+                         "note": "achieved = SURVEY §8d algorithmic flops of this GPU's batch ÷ HIP-event time of its "
+                                 "launches on the library stream; the §8d count is for the capacitance form, this "
+                                 "build's collapsed form executes about half of it (executed_* = PMC-counted FP64 "
+                                 "flops of the same launch from profiles/, which is why frac can exceed 1)"},
             "cpu_baseline": cpu,
             "outputs": {"neg_inf": n_neginf, "nan": n_nan},
         }
