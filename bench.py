@@ -175,13 +175,13 @@ def cpu_baseline(w: Workload, seconds: float, gpu_out: np.ndarray):
 
 
 def pmc_executed_flops(kernel_substr: str):
-    """Executed FP64 flops per eval of the dominant kernel from the committed PMC valu pass:
+    """Executed FP64 flops per filter step of the dominant kernel from the committed PMC valu pass (T = 600):
     (FMA·2 + ADD + MUL)·64 + MFMA_MOPS_F64·512 (the expression of rocprof's SQ_INSTS_VALU_FLOPS_FP64)."""
     for rnd in sorted((ROOT / "profiles").glob("r*/**/pmc_summary.json"), reverse=True):
         d = json.loads(rnd.read_text())
         for k, v in d.items():
-            if kernel_substr in k and "fp64_flops_executed_per_eval" in v:
-                return v["fp64_flops_executed_per_eval"]
+            if kernel_substr in k and "fp64_flops_executed_per_step" in v:
+                return v["fp64_flops_executed_per_step"]
     return None
 
 
@@ -306,7 +306,8 @@ def main():
     achieved = f_rank / (kernel_ms * 1e-3) / 1e12  # TFLOP/s of this GPU's launches
     traffic, traffic_src = pmc_traffic(DOMINANT[kind])
     exe = pmc_executed_flops(DOMINANT[kind])
-    exe_tf = exe * B / (kernel_ms * 1e-3) / 1e12 if exe else None
+    steps = float(np.sum(w.T_use - 1)) if w.T_use is not None else float(B * (T - 1))
+    exe_tf = exe * steps / (kernel_ms * 1e-3) / 1e12 if exe else None
     out_host = d_out.cpu().numpy()
     n_neginf, n_nan = int(np.isneginf(out_host).sum()), int(np.isnan(out_host).sum())
 
