@@ -207,3 +207,34 @@ def test_model_api_predict(engine, panel):
     for k in KEYS:
         assert_close(r[k], ref[k], what=k)
     assert r["preds"].shape == (30, 80) and r["factors"].shape == (3, 80)
+
+
+def test_trajectory_api_errors(engine, panel):
+    """Invalid requests return the documented status and message (include/yfm.h), never a kernel."""
+    import ctypes
+    from yfm_amd import _lib
+    Y, mats = panel
+    engine.set_panel(Y[:, :30], mats)
+    lib = engine.lib
+    th = np.ascontiguousarray(np.tile(S.theta0_constrained(KIND_DNS)[:, None], (1, 2)).T)
+    out = np.zeros(4096)
+    D = _lib.dptr
+    assert lib.yfm_predict(engine.ctx, 0, 1, D(th), 20, 2, None, 0, D(out), D(out), D(out), None, None) == -1
+    assert b"horizon" in lib.yfm_last_error()
+    assert lib.yfm_forecast(engine.ctx, 0, 1, D(th), 20, 2, None, 0, D(out)) == -1
+    assert lib.yfm_loss_array(engine.ctx, 0, 1, D(th), 20, 2, None, 0, D(out)) == -1
+    tu = np.array([10, 20], dtype=np.int32)
+    assert lib.yfm_loss_array(engine.ctx, 0, 1, D(th), 20, 2, _lib.iptr(tu), 2, D(out)) == -4  # EUNSUPPORTED
+    assert lib.yfm_predict(engine.ctx, 0, 1, D(th), 19, 2, None, 1, D(out), D(out), D(out), None, None) == -1
+    bad = np.array([0, 5], dtype=np.int32)
+    assert lib.yfm_forecast(engine.ctx, 0, 1, D(th), 20, 2, _lib.iptr(bad), 2, D(out)) == -1
+    st = np.zeros(2, dtype=np.int32)
+    ll = np.zeros(2)
+    assert lib.yfm_estimate(engine.ctx, 0, 1, D(th), 20, 2, None, 10, 1e-6, 0, 1e-8, D(out), None, D(ll),
+                            _lib.iptr(st), None) == -1  # max_group_iters < 1
+    assert lib.yfm_estimate(engine.ctx, 0, 5, D(th), 20, 2, None, 10, 1e-6, 1, 1e-8, D(out), None, D(ll),
+                            _lib.iptr(st), None) == -1  # param_space
+    assert lib.yfm_gamma_dim(0) == 1 and lib.yfm_gamma_dim(1) == 1 and lib.yfm_gamma_dim(2) == 2
+    assert lib.yfm_gamma_dim(7) == -1
+    # B = 0 is a valid empty request
+    assert lib.yfm_predict(engine.ctx, 0, 1, D(th), 20, 0, None, 1, D(out), D(out), D(out), None, None) == 0
