@@ -311,6 +311,21 @@ def main():
     out_host = d_out.cpu().numpy()
     n_neginf, n_nan = int(np.isneginf(out_host).sum()), int(np.isnan(out_host).sum())
 
+    # host-pointer boundary (yfm_loglik_batch: θ in over PCIe, logliks back, synchronous) —
+    # reported beside the metric, never as `value` (inputs are not HBM-resident there)
+    host_rate = None
+    if rank == 0 and world == 1:
+        Th_host = np.asfortranarray(w.Theta)
+        tu_host = w.T_use
+        eng.loglik(kind, Th_host, space=0, T_use=tu_host)
+        reps = max(3, min(args.steps, 10))
+        th0 = time.perf_counter()
+        for _ in range(reps):
+            eng.loglik(kind, Th_host, space=0, T_use=tu_host)
+        host_s = (time.perf_counter() - th0) / reps
+        host_rate = {"evals_per_s": B / host_s, "ms_per_call": 1e3 * host_s, "calls": reps,
+                     "note": "yfm_loglik_batch with host θ / host logliks (H2D + kernel + D2H, synchronous)"}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(w, args.cpu_seconds, out_host)
@@ -344,6 +359,7 @@ def main():
                                  "build's collapsed form executes about half of it (executed_* = PMC-counted FP64 "
                                  "flops of the same launch from profiles/, which is why frac can exceed 1)"},
             "cpu_baseline": cpu,
+            "host_pointer_rate": host_rate,
             "outputs": {"neg_inf": n_neginf, "nan": n_nan},
         }
         print(json.dumps(line), flush=True)

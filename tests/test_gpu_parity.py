@@ -11,6 +11,7 @@ import pytest
 from conftest import GOLDEN_NAMES, ROOT, load_golden
 from yfm_amd import KIND_DNS, KIND_GNS, KIND_TVL, _lib
 from yfm_amd import synthetic as S
+from yfm_amd.params import n_params
 
 pytestmark = pytest.mark.gpu
 
@@ -174,6 +175,31 @@ def test_device_pointer_api_matches_host_api(engine, headline):
     engine.loglik_device(KIND_DNS, dth.data_ptr(), 20, 4096, out.data_ptr(), space=0, stream=s.cuda_stream)
     s.synchronize()
     np.testing.assert_array_equal(out.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("kind", [KIND_DNS, KIND_GNS])
+def test_pipelined_host_batch_matches_device_launch(engine, headline, kind):
+    """B ≥ 2×131,072: yfm_loglik_batch uploads θ in chunks on a copy stream while earlier chunks
+    run; the logliks equal one device-pointer launch bit for bit, with ragged T_use windows, and
+    the flag counters cover every chunk."""
+    import torch
+    Y, mats = headline
+    engine.set_panel(Y[:, :120], mats)
+    B = 300_001  # three chunks, the last one ragged
+    P = n_params(kind)
+    Th = S.theta_batch(kind, B, seed=31, bad_frac=0.05)
+    tu = np.random.default_rng(5).integers(2, 121, B).astype(np.int32)
+    got = engine.loglik(kind, Th, T_use=tu)
+    n_throw, n_neginf = engine.last_flags()
+    assert n_throw == np.isnan(got).sum() and n_neginf == np.isneginf(got).sum()
+    dth = torch.from_numpy(np.ascontiguousarray(Th.T)).cuda()
+    dtu = torch.from_numpy(tu).cuda()
+    out = torch.empty(B, dtype=torch.float64, device="cuda")
+    s = torch.cuda.current_stream()
+    engine.loglik_device(kind, dth.data_ptr(), P, B, out.data_ptr(), space=0, d_T_use=dtu.data_ptr(),
+                         stream=s.cuda_stream)
+    s.synchronize()
+    np.testing.assert_array_equal(got, out.cpu().numpy())
 
 
 def test_windows_share_prefix(engine, headline):

@@ -6,6 +6,7 @@
 // and a missing/failed device is reported as an error.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -71,6 +72,7 @@ struct DevBuf {
 struct yfm_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t copy_stream = nullptr;  // θ uploads of pipelined host-pointer batches (created lazily)
   // panel
   int N = 0, T = 0, np = 0, ldp = 0;
   DevBuf panel, mats, raw;
@@ -88,6 +90,10 @@ struct yfm_ctx {
 };
 
 namespace {
+
+// host-pointer pipelining (yfm_loglik_batch): chunk ≥ 2 per-lane waves per SIMD, ≤ 8 chunks
+constexpr int kPipeChunk = 131072;
+constexpr int kPipeMaxChunks = 8;
 
 int check_ctx(yfm_ctx* ctx) {
   if (!ctx) return set_error(YFM_EINVAL, "null context");
@@ -168,8 +174,8 @@ struct PanelView {
 
 int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int B, const int* d_T_use,
            double* d_out, double* d_rb, double* d_rP, hipStream_t s, int horizon = 0, int rec_len = 0,
-           const PanelView* pv = nullptr) {
-  YFM_HIP_CHECK(hipMemsetAsync(ctx->flags.p, 0, 2 * sizeof(unsigned int), s));
+           const PanelView* pv = nullptr, bool reset_flags = true) {
+  if (reset_flags) YFM_HIP_CHECK(hipMemsetAsync(ctx->flags.p, 0, 2 * sizeof(unsigned int), s));
   if (B == 0) return YFM_OK;
   yfm::LaunchArgs a;
   a.theta = d_theta;
@@ -343,6 +349,7 @@ void yfm_destroy(yfm_ctx* ctx) {
   for (DevBuf* b : {&ctx->traj, &ctx->init_bad, &ctx->tiled_raw, &ctx->tiled_panel, &ctx->defer}) b->release();
   for (DevBuf& b : ctx->gap_buf) b.release();
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
   delete ctx;
 }
 
@@ -379,20 +386,59 @@ int yfm_loglik_batch(yfm_ctx* ctx, int model_kind, int param_space, const double
   const size_t nb = (size_t)(B > 0 ? B : 1);
   YFM_HIP_CHECK(ctx->theta.ensure(sizeof(double) * (size_t)P * nb));
   YFM_HIP_CHECK(ctx->out.ensure(sizeof(double) * nb));
-  if (B > 0)
-    YFM_HIP_CHECK(hipMemcpyAsync(ctx->theta.p, theta, sizeof(double) * (size_t)P * B, hipMemcpyHostToDevice,
-                                 ctx->stream));
-  const int* d_tuse = nullptr;
-  if (T_use && B > 0) {
-    YFM_HIP_CHECK(ctx->tuse.ensure(sizeof(int) * nb));
-    YFM_HIP_CHECK(hipMemcpyAsync(ctx->tuse.p, T_use, sizeof(int) * B, hipMemcpyHostToDevice, ctx->stream));
-    d_tuse = static_cast<const int*>(ctx->tuse.p);
+  if (T_use && B > 0) YFM_HIP_CHECK(ctx->tuse.ensure(sizeof(int) * nb));
+  double* d_th = static_cast<double*>(ctx->theta.p);
+  double* d_out = static_cast<double*>(ctx->out.p);
+  int* d_tu = T_use ? static_cast<int*>(ctx->tuse.p) : nullptr;
+  // Batches that fill the chip several times over are pipelined: chunk k+1's θ is uploaded on
+  // the copy stream while chunk k's filter runs on the context stream (each chunk still holds
+  // ≥ 2 waves per SIMD of candidates).  Evaluations are independent, so the logliks are the
+  // same bits as one launch; the flags accumulate over the chunks.
+  int chunk = B;
+  if (model_kind != YFM_MODEL_TVL && B >= 2 * kPipeChunk) {
+    chunk = std::max(kPipeChunk, (B + kPipeMaxChunks - 1) / kPipeMaxChunks);
+    if (!ctx->copy_stream) YFM_HIP_CHECK(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
   }
-  if (int r = launch(ctx, model_kind, param_space, static_cast<const double*>(ctx->theta.p), P, B, d_tuse,
-                     static_cast<double*>(ctx->out.p), nullptr, nullptr, ctx->stream))
+  if (chunk < B) {
+    const int nchunks = (B + chunk - 1) / chunk;
+    std::vector<hipEvent_t> ev(nchunks, nullptr);
+    int rc = YFM_OK;
+    for (int k = 0; k < nchunks && rc == YFM_OK; ++k) {
+      const int b0 = k * chunk, nbk = std::min(chunk, B - b0);
+      hipError_t e = hipEventCreateWithFlags(&ev[k], hipEventDisableTiming);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(d_th + (size_t)P * b0, theta + (size_t)P * b0, sizeof(double) * (size_t)P * nbk,
+                           hipMemcpyHostToDevice, ctx->copy_stream);
+      if (e == hipSuccess && d_tu)
+        e = hipMemcpyAsync(d_tu + b0, T_use + b0, sizeof(int) * nbk, hipMemcpyHostToDevice, ctx->copy_stream);
+      if (e == hipSuccess) e = hipEventRecord(ev[k], ctx->copy_stream);
+      if (e == hipSuccess) e = hipStreamWaitEvent(ctx->stream, ev[k], 0);
+      if (e != hipSuccess) {
+        rc = set_error(YFM_EHIP, "pipelined upload: %s", hipGetErrorString(e));
+        break;
+      }
+      rc = launch(ctx, model_kind, param_space, d_th + (size_t)P * b0, P, nbk, d_tu ? d_tu + b0 : nullptr,
+                  d_out + b0, nullptr, nullptr, ctx->stream, 0, 0, nullptr, k == 0);
+    }
+    if (rc == YFM_OK) {
+      hipError_t e = hipMemcpyAsync(loglik_out, d_out, sizeof(double) * B, hipMemcpyDeviceToHost, ctx->stream);
+      if (e != hipSuccess) rc = set_error(YFM_EHIP, "hipMemcpyAsync: %s", hipGetErrorString(e));
+    }
+    (void)hipStreamSynchronize(ctx->copy_stream);
+    hipError_t e = hipStreamSynchronize(ctx->stream);
+    for (hipEvent_t x : ev)
+      if (x) (void)hipEventDestroy(x);
+    if (rc == YFM_OK && e != hipSuccess) rc = set_error(YFM_EHIP, "hipStreamSynchronize: %s", hipGetErrorString(e));
+    return rc;
+  }
+  if (B > 0)
+    YFM_HIP_CHECK(hipMemcpyAsync(d_th, theta, sizeof(double) * (size_t)P * B, hipMemcpyHostToDevice, ctx->stream));
+  if (d_tu && B > 0)
+    YFM_HIP_CHECK(hipMemcpyAsync(d_tu, T_use, sizeof(int) * B, hipMemcpyHostToDevice, ctx->stream));
+  if (int r = launch(ctx, model_kind, param_space, d_th, P, B, d_tu, d_out, nullptr, nullptr, ctx->stream))
     return r;
   if (B > 0)
-    YFM_HIP_CHECK(hipMemcpyAsync(loglik_out, ctx->out.p, sizeof(double) * B, hipMemcpyDeviceToHost, ctx->stream));
+    YFM_HIP_CHECK(hipMemcpyAsync(loglik_out, d_out, sizeof(double) * B, hipMemcpyDeviceToHost, ctx->stream));
   YFM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
   return YFM_OK;
 }
