@@ -205,8 +205,8 @@ DOMINANT = {KIND_DNS: "fixedz_loglik_kernel<30, 3, 1, false>", KIND_TVL: "tvl_lo
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
     ap.add_argument("--batch", type=int, default=None, help="θ per GPU (2, 3), per window (4), total (5)")
     ap.add_argument("--T", type=int, default=600)

@@ -13,5 +13,5 @@ timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/
 echo "smoke ok"
 timeout -k 10 200 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
 cat "$OUT/bench.json"
-timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/bench_traced.json" 2> "$OUT/prof.err"
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --no-cpu-baseline > "$OUT/bench_traced.json" 2> "$OUT/prof.err"
 echo "rocprof ok"

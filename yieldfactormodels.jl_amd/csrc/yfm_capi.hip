@@ -78,10 +78,10 @@ struct yfm_ctx {
   DevBuf panel, mats, raw;
   // staging for host-pointer calls
   DevBuf theta, out, tuse, rec_beta, rec_P;
-  DevBuf flags;  // 2 × unsigned int
+  DevBuf flags;  // 4 × unsigned int: n_init_throw, n_neg_inf, deferred-candidate count, pad
   DevBuf scratch;  // per-candidate work records (TVλ init)
   DevBuf traj, init_bad;       // trajectory-mode state records, per-candidate init-throw marks
-  DevBuf defer;                // [count, list...] of candidates handed from the per-lane to the group kernel
+  DevBuf defer;                // list of candidates handed from the per-lane to the group kernel
   DevBuf tiled_raw, tiled_panel;  // get_loss_array with K > 1 passes: the panel tiled K times
   // TVλ maturity-jump tables, one per lane count L = 2^l (built lazily, reset by set_panel)
   std::vector<double> mats_host;
@@ -175,7 +175,12 @@ struct PanelView {
 int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int B, const int* d_T_use,
            double* d_out, double* d_rb, double* d_rP, hipStream_t s, int horizon = 0, int rec_len = 0,
            const PanelView* pv = nullptr, bool reset_flags = true) {
-  if (reset_flags) YFM_HIP_CHECK(hipMemsetAsync(ctx->flags.p, 0, 2 * sizeof(unsigned int), s));
+  // one fill resets the flag counters (unless a pipelined chunk continues them) and the
+  // deferred-candidate count: flags.p = [n_init_throw, n_neg_inf, defer_count, pad]
+  {
+    unsigned int* f = static_cast<unsigned int*>(ctx->flags.p);
+    YFM_HIP_CHECK(hipMemsetAsync(reset_flags ? f : f + 2, 0, (reset_flags ? 3 : 1) * sizeof(unsigned int), s));
+  }
   if (B == 0) return YFM_OK;
   yfm::LaunchArgs a;
   a.theta = d_theta;
@@ -219,10 +224,9 @@ int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int 
     // N ≤ 64: one filter per lane (MFMA Z'y), then the lane-group kernel for the candidates it
     // deferred (ill-conditioned Z'Z); larger N: one filter per lane group for every candidate
     if (yfm::fixedz_np_for(ctx->N) > 0) {
-      YFM_HIP_CHECK(ctx->defer.ensure(sizeof(int) * ((size_t)B + 1)));
-      a.defer_count = static_cast<int*>(ctx->defer.p);
-      a.defer_list = a.defer_count + 1;
-      YFM_HIP_CHECK(hipMemsetAsync(a.defer_count, 0, sizeof(int), s));
+      YFM_HIP_CHECK(ctx->defer.ensure(sizeof(int) * (size_t)B));
+      a.defer_count = reinterpret_cast<int*>(static_cast<unsigned int*>(ctx->flags.p) + 2);  // zeroed above
+      a.defer_list = static_cast<int*>(ctx->defer.p);
       e = yfm::launch_fixedz(kind, a);
       if (e == hipSuccess) e = yfm::launch_fixedz_group(kind, a);
     } else {
@@ -330,12 +334,12 @@ yfm_ctx* yfm_create(int hip_device) {
   yfm_ctx* ctx = new yfm_ctx();
   ctx->device = hip_device;
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
-      ctx->flags.ensure(2 * sizeof(unsigned int)) != hipSuccess) {
+      ctx->flags.ensure(4 * sizeof(unsigned int)) != hipSuccess) {
     set_error(YFM_EHIP, "context allocation failed on device %d", hip_device);
     yfm_destroy(ctx);
     return nullptr;
   }
-  (void)hipMemset(ctx->flags.p, 0, 2 * sizeof(unsigned int));
+  (void)hipMemset(ctx->flags.p, 0, 4 * sizeof(unsigned int));
   return ctx;
 }
 
