@@ -28,18 +28,29 @@ static void run(int blocks_per_cu, const char* tag) {
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   fma_loop<ACC><<<blocks, 256>>>(d, 100, 0.999999, 1e-7);
-  hipEventRecord(e0);
-  fma_loop<ACC><<<blocks, 256>>>(d, iters, 0.999999, 1e-7);
-  hipEventRecord(e1);
-  hipEventSynchronize(e1);
-  float ms;
-  hipEventElapsedTime(&ms, e0, e1);
+  float ms = 1e30f;
+  for (int rep = 0; rep < 5; ++rep) {  // best of 5 (clocks settle after the ramp in main)
+    float m;
+    hipEventRecord(e0);
+    fma_loop<ACC><<<blocks, 256>>>(d, iters, 0.999999, 1e-7);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    hipEventElapsedTime(&m, e0, e1);
+    if (m < ms) ms = m;
+  }
   const double flops = 2.0 * ACC * (double)iters * blocks * 256;
   printf("%-28s ACC=%2d blocks/CU=%d  %.2f TFLOP/s\n", tag, ACC, blocks_per_cu, flops / (ms * 1e-3) / 1e12);
   hipFree(d);
 }
 
 int main() {
+  {  // ≈0.2 s of full-chip FMA work first, so the card is at its steady clock when timed
+    double* d;
+    hipMalloc(&d, 8);
+    for (int k = 0; k < 4; ++k) fma_loop<16><<<256 * 8, 256>>>(d, 200000, 0.999999, 1e-7);
+    hipDeviceSynchronize();
+    hipFree(d);
+  }
   run<16>(1, "1 wave/SIMD");
   run<8>(1, "1 wave/SIMD");
   run<4>(1, "1 wave/SIMD");
