@@ -38,6 +38,26 @@
 
 namespace {
 
+// Page-locked host staging for the per-round batch: the runtime DMAs straight from it
+// instead of bouncing pageable memory through its own buffer (one round trip per round).
+struct PinnedBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    const size_t want = std::max(bytes, cap * 2);
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  ~PinnedBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+};
+
 enum Code { ID = 0, POS = 1, R11 = 2 };
 
 // transform vectors: kalmanbasemodel.jl:74-120 (+ dns.jl:15-22 one leading γ; GNS5 two)
@@ -364,6 +384,7 @@ extern "C" int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const
   }
   std::vector<double> batch, out;
   std::vector<int> tuse;
+  PinnedBuf pin_th, pin_tu, pin_out;
   long long evals = 0;
   for (;;) {
     batch.clear();
@@ -372,9 +393,17 @@ extern "C" int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const
     const int B = (int)(batch.size() / P);
     if (B == 0) break;
     out.resize(B);
-    const int rc = yfm_loglik_batch(ctx, model_kind, YFM_THETA_UNCONSTRAINED, batch.data(), P, B,
-                                    T_use ? tuse.data() : nullptr, out.data());
+    if (pin_th.ensure(sizeof(double) * batch.size()) != hipSuccess ||
+        pin_out.ensure(sizeof(double) * (size_t)B) != hipSuccess ||
+        (T_use && pin_tu.ensure(sizeof(int) * (size_t)B) != hipSuccess))
+      return yfm::api_error(YFM_EHIP, "hipHostMalloc failed for the estimation batch");
+    std::memcpy(pin_th.p, batch.data(), sizeof(double) * batch.size());
+    if (T_use) std::memcpy(pin_tu.p, tuse.data(), sizeof(int) * (size_t)B);
+    const int rc = yfm_loglik_batch(ctx, model_kind, YFM_THETA_UNCONSTRAINED, static_cast<const double*>(pin_th.p),
+                                    P, B, T_use ? static_cast<const int*>(pin_tu.p) : nullptr,
+                                    static_cast<double*>(pin_out.p));
     if (rc != YFM_OK) return rc;
+    std::memcpy(out.data(), pin_out.p, sizeof(double) * (size_t)B);
     evals += B;
     for (double& v : out) v = -v;  // compute_loss = −loglik (optimization.jl:22)
     for (Chain& c : chains)
