@@ -383,8 +383,8 @@ int tvl_max_n() { return (kTvlPre * kTvlBlock) - 1; }
 
 int tvl_lanes_for(int B, int N) {
   // enough lanes for two waves per SIMD (256 CUs × 4 SIMDs × 2 × 64 lanes — the kernel is
-  // built for two; measured on MI355X at N = 360: B = 16,384 → L = 8 (5.98 ms vs 6.11 ms at
-  // L = 4), B = 65,536 → L = 2), capped at a wave and at the maturity count rounded up to a
+  // built for two; measured on MI355X at N = 360: B = 16,384 → L = 8 (5.77 ms vs 6.06 ms at
+  // L = 4 and 7.65 ms at L = 16, steady clock, profiles/r1/final/tvl_lanes), B = 65,536 → L = 2), capped at a wave and at the maturity count rounded up to a
   // power of two
   long long want = (2048LL * 64 + B - 1) / (B > 0 ? B : 1);
   int L = 1;
