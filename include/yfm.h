@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define YFM_ABI_VERSION 1
+#define YFM_ABI_VERSION 2
 
 typedef struct yfm_ctx yfm_ctx;
 
@@ -58,6 +58,17 @@ enum yfm_status {
   YFM_EUNSUPPORTED = -4 /* valid request this build has no kernel for */
 };
 
+/* precision — arithmetic of the TVλ EKF (the fixed-loading models always run FP64: their
+ * filter is contracting and the collapsed form is within 1e-12 of exact arithmetic)
+ *   YFM_PREC_FP64  FP64 throughout (the reference's own arithmetic class; fastest).
+ *   YFM_PREC_DD    double-double (~106-bit) recursion: for candidates whose EKF amplifies
+ *                  rounding by 1e10..1e13 (no FP64 evaluation, the reference's included, is
+ *                  then within 1e-9 of the exact value) the result stays ~1e-20 from it.
+ *   YFM_PREC_AUTO  FP64, then a second FP64 evaluation with a different summation order and
+ *                  initialisation rounding; candidates whose two values differ by more than
+ *                  1e-13 relative are re-evaluated in double-double. */
+enum yfm_precision { YFM_PREC_FP64 = 0, YFM_PREC_DD = 1, YFM_PREC_AUTO = 2 };
+
 /* Library/ABI introspection. */
 int yfm_abi_version(void);
 /* Length P of θ for a model kind (kalmanbasemodel.jl:106-112 + dns.jl:15-22). */
@@ -71,6 +82,11 @@ const char* yfm_last_error(void);
  * KalmanBaseModel (kalmanbasemodel.jl:46-130): device buffers live in the ctx. */
 yfm_ctx* yfm_create(int hip_device);
 void yfm_destroy(yfm_ctx* ctx);
+
+/* Select the TVλ arithmetic for subsequent calls on this context (default YFM_PREC_FP64).
+ * The reference has no such switch: its Float64 path is YFM_PREC_FP64's arithmetic class. */
+int yfm_set_precision(yfm_ctx* ctx, int precision);
+int yfm_get_precision(yfm_ctx* ctx);
 
 /* Upload the yield panel.  Y: N×T column-major (the `data` argument of get_loss,
  * filter.jl:182); maturities: N (KalmanBaseModel.maturities).  Copied; the

@@ -214,3 +214,41 @@ def test_loss_array_passes_continue_the_state():
     Yt = np.hstack([Y[:, :29], Y])
     one = O.get_loss_array(_state(KIND_DNS, mats, th), Yt, K=1)
     np.testing.assert_allclose(2 * two, one[:29] + np.concatenate([[0.0], one[30:]]), rtol=1e-12)
+
+
+# ---- the binary128 truth (oracle/yfm_truth.c) used to adjudicate parity -----------------
+@pytest.mark.parametrize("name", [n for n in GOLDEN_NAMES if "ll_truth" in load_golden(n)])
+def test_quad_truth_pinned_to_mp_dense_truth(name):
+    """The quad-precision capacitance-form truth equals the 40-digit DENSE restatement
+    (oracle/kalman_mp.py: F = ZPZ' + σ²I formed and inverted as filter.jl does) on every
+    golden fixture that carries one — loglik to the last bit of the FP64 rounding, the state
+    trajectories to a few ulps."""
+    from oracle.truth import loglik_truth, states_truth
+    g = load_golden(name)
+    kind = int(g["kind"])
+    k = len(g["ll_truth"])
+    tu = None if "T_use" not in g else g["T_use"][:k]
+    got = loglik_truth(kind, g["Y"], g["maturities"], g["Theta"][:, :k], space=int(g["space"]), T_use=tu)
+    assert rel_err(got, g["ll_truth"]) <= 2e-16
+    if "beta_truth" in g:
+        for b in range(g["beta_truth"].shape[-1]):
+            if not np.isfinite(g["loglik"][b]):
+                continue
+            _, beta, P = states_truth(kind, g["Y"], g["maturities"], g["Theta"][:, b], space=int(g["space"]))
+            for a, t in ((beta, g["beta_truth"][..., b]), (P, g["P_truth"][..., b])):
+                assert np.abs(a - t).max() <= 4e-16 * np.abs(t).max()
+
+
+def test_quad_truth_tvl_n360_summation_order_invariant():
+    """At the config-3 cross-section (N = 360) the truth does not depend on its own rounding: the
+    same candidates with the maturities (and panel rows) in reverse order — every sum over
+    maturities taken in the opposite order — agree to 1e-15 even where the EKF amplifies an FP64
+    rounding to 1e-4 (candidates chosen from the config-3 batch by that property)."""
+    from oracle.truth import loglik_truth
+    mats = S.maturities_360()
+    Y = S.simulate_panel(KIND_TVL, 600, maturities=mats)
+    Th = S.theta_batch(KIND_TVL, 16384, seed=S.BATCH_SEED, bad_frac=0.0, scale=0.02)[:, [32, 34, 44, 0]]
+    a = loglik_truth(KIND_TVL, Y, mats, Th)
+    b = loglik_truth(KIND_TVL, Y[::-1], mats[::-1], Th)
+    assert np.all(np.isfinite(a))
+    assert rel_err(a, b) <= 1e-15

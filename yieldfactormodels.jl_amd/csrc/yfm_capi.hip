@@ -71,6 +71,7 @@ struct DevBuf {
 
 struct yfm_ctx {
   int device = 0;
+  int precision = YFM_PREC_FP64;  // TVλ arithmetic (yfm_set_precision)
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;  // θ uploads of pipelined host-pointer batches (created lazily)
   // panel
@@ -215,11 +216,21 @@ int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int 
       const int l = std::atoi(ov);
       if (l >= 1 && l <= 64 && (l & (l - 1)) == 0) lanes = l;
     }
-    YFM_HIP_CHECK(ctx->scratch.ensure(yfm::tvl_scratch_bytes(B)));
-    a.scratch = static_cast<double*>(ctx->scratch.p);
-    yfm::TvlGaps g;
-    if (int r = tvl_gaps(ctx, lanes, g)) return r;
-    e = yfm::launch_tvl(a, g, lanes);
+    if (ctx->precision == YFM_PREC_DD) {
+      if (!std::getenv("YFM_TVL_LANES")) lanes = yfm::tvl_dd_lanes_for(B, ctx->N);
+      YFM_HIP_CHECK(ctx->scratch.ensure(yfm::tvl_dd_scratch_bytes(B)));
+      a.scratch = static_cast<double*>(ctx->scratch.p);
+      yfm::TvlGaps g;
+      if (int r = tvl_gaps(ctx, lanes, g)) return r;
+      e = yfm::launch_tvl_dd_init(a);
+      if (e == hipSuccess) e = yfm::launch_tvl_dd(a, g, lanes, nullptr);
+    } else {
+      YFM_HIP_CHECK(ctx->scratch.ensure(yfm::tvl_scratch_bytes(B)));
+      a.scratch = static_cast<double*>(ctx->scratch.p);
+      yfm::TvlGaps g;
+      if (int r = tvl_gaps(ctx, lanes, g)) return r;
+      e = yfm::launch_tvl(a, g, lanes);
+    }
   } else {
     // N ≤ 64: one filter per lane (MFMA Z'y), then the lane-group kernel for the candidates it
     // deferred (ill-conditioned Z'Z); larger N: one filter per lane group for every candidate
@@ -355,6 +366,19 @@ void yfm_destroy(yfm_ctx* ctx) {
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
   delete ctx;
+}
+
+int yfm_set_precision(yfm_ctx* ctx, int precision) {
+  if (int r = check_ctx(ctx)) return r;
+  if (precision != YFM_PREC_FP64 && precision != YFM_PREC_DD && precision != YFM_PREC_AUTO)
+    return set_error(YFM_EINVAL, "unknown precision %d", precision);
+  ctx->precision = precision;
+  return YFM_OK;
+}
+
+int yfm_get_precision(yfm_ctx* ctx) {
+  if (!ctx) return set_error(YFM_EINVAL, "null context");
+  return ctx->precision;
 }
 
 int yfm_set_panel(yfm_ctx* ctx, const double* Y, int N, int T, const double* maturities) {

@@ -1,0 +1,153 @@
+// yfm_dd.hpp — double-double ("dd", ~106-bit significand) arithmetic on the FP64 VALU,
+// for the certified TVλ path (yfm_tvl_dd.hip).
+//
+// Why it exists: a sizeable share of TVλ EKF candidates amplify any FP64 rounding by
+// 1e10..1e13 over T = 600 steps (the reference's dZ1 Jacobian makes the filter locally
+// expanding), so every FP64 implementation of filter.jl:12-80 — the reference's own dense
+// path included — lands up to 1e-4 away from the exact-arithmetic value, and two such
+// implementations disagree by as much.  Carrying the recursion in dd makes the kernel's
+// local error ~1e-32 instead of ~1e-16, so its result sits orders of magnitude closer to
+// exact arithmetic than any FP64 evaluation.
+//
+// Algorithms: error-free transformations (Knuth TwoSum, Dekker FastTwoSum, FMA TwoProd)
+// and the double-word operations of Joldes, Muller & Popescu (ACM TOMS 2017):
+// DWTimesDW (relative error ≤ 5u²), DWPlusFP, and a "sloppy" DW+DW whose ABSOLUTE error is
+// ≤ ~3u²(|x|+|y|) — the bound the filter needs (an accumulation error small against the
+// operands, like exact-arithmetic summation up to 2^-104).
+#pragma once
+#include <hip/hip_runtime.h>
+
+// Floating-point contraction must stay off in every translation unit that includes this
+// header (a fused a·b + c inside TwoSum / TwoProd would break the error-free
+// transformations); the pragma below covers the rest of the including file.
+#pragma clang fp contract(off)
+
+namespace yfm {
+
+struct dd {
+  double hi, lo;
+};
+
+__device__ __forceinline__ dd dd_make(double x) { return {x, 0.0}; }
+
+// s + e = a + b exactly (any magnitudes)
+__device__ __forceinline__ dd two_sum(double a, double b) {
+  const double s = a + b;
+  const double bb = s - a;
+  const double e = (a - (s - bb)) + (b - bb);
+  return {s, e};
+}
+// s + e = a + b exactly, requires |a| ≥ |b| (or a = 0)
+__device__ __forceinline__ dd fast_two_sum(double a, double b) {
+  const double s = a + b;
+  return {s, b - (s - a)};
+}
+// p + e = a·b exactly
+__device__ __forceinline__ dd two_prod(double a, double b) {
+  const double p = a * b;
+  return {p, __builtin_fma(a, b, -p)};
+}
+
+__device__ __forceinline__ dd dd_neg(dd x) { return {-x.hi, -x.lo}; }
+
+// x + y, absolute error ≤ ~3u²(|x| + |y|)
+__device__ __forceinline__ dd dd_add(dd x, dd y) {
+  dd s = two_sum(x.hi, y.hi);
+  s.lo += x.lo + y.lo;
+  return fast_two_sum(s.hi, s.lo);
+}
+__device__ __forceinline__ dd dd_sub(dd x, dd y) { return dd_add(x, dd_neg(y)); }
+// x + d (d a double)
+__device__ __forceinline__ dd dd_add_d(dd x, double d) {
+  dd s = two_sum(x.hi, d);
+  s.lo += x.lo;
+  return fast_two_sum(s.hi, s.lo);
+}
+// x·y, relative error ≤ 5u²
+__device__ __forceinline__ dd dd_mul(dd x, dd y) {
+  dd p = two_prod(x.hi, y.hi);
+  p.lo = __builtin_fma(x.hi, y.lo, __builtin_fma(x.lo, y.hi, p.lo));
+  return fast_two_sum(p.hi, p.lo);
+}
+// x·d
+__device__ __forceinline__ dd dd_mul_d(dd x, double d) {
+  dd p = two_prod(x.hi, d);
+  p.lo = __builtin_fma(x.lo, d, p.lo);
+  return fast_two_sum(p.hi, p.lo);
+}
+// exact scaling by a power of two
+__device__ __forceinline__ dd dd_ldexp(dd x, int k) { return {__builtin_ldexp(x.hi, k), __builtin_ldexp(x.lo, k)}; }
+// 1 / y: FP64 seed + one Newton step in dd (relative error ~ u²)
+__device__ __forceinline__ dd dd_rcp(dd y) {
+  const double r0 = 1.0 / y.hi;
+  const dd e = dd_add_d(dd_neg(dd_mul_d(y, r0)), 1.0);  // 1 − y·r0
+  return dd_add_d(dd_mul_d(e, r0), r0);                  // r0 + r0·e
+}
+__device__ __forceinline__ dd dd_div(dd x, dd y) { return dd_mul(x, dd_rcp(y)); }
+__device__ __forceinline__ double dd_to_double(dd x) { return x.hi + x.lo; }
+
+// Accumulator with deferred normalisation: Σ terms kept as an exact leading sum (TwoSum) and
+// a plain FP64 sum of all trailing parts.  Same accuracy class as repeated dd_add for the
+// sums here (≤ a few hundred terms), at 8 ops per dd term instead of 11.
+struct dd_acc {
+  double hi = 0.0, lo = 0.0;
+  __device__ __forceinline__ void add(dd x) {
+    const dd s = two_sum(hi, x.hi);
+    hi = s.hi;
+    lo += s.lo + x.lo;
+  }
+  // += a·b without normalising the product
+  __device__ __forceinline__ void add_prod(dd a, dd b) {
+    dd p = two_prod(a.hi, b.hi);
+    p.lo = __builtin_fma(a.hi, b.lo, __builtin_fma(a.lo, b.hi, p.lo));
+    add(p);
+  }
+  __device__ __forceinline__ dd value() const { return two_sum(hi, lo); }  // |lo| may exceed |hi| after cancellation
+};
+
+// exp of a dd argument to ~2u² relative: x = k·ln2 + r, |r| ≤ ln2/2, e^r from a degree-9
+// Taylor polynomial of r/2^9 followed by 9 squarings of (1 + s) carried as s ← s(2 + s).
+// Arguments beyond the FP64 range give 0 / Inf like exp(); NaN propagates.
+__device__ __forceinline__ dd dd_exp(dd x) {
+  constexpr double kLn2Hi = 0.6931471805599453094172321214581766;  // nearest double to ln 2
+  constexpr double kLn2Lo = 2.3190468138462996154e-17;             // ln 2 − kLn2Hi
+  if (!(x.hi > -745.2)) return {x.hi != x.hi ? x.hi : 0.0, 0.0};
+  if (x.hi > 709.8) return {__builtin_inf(), 0.0};
+  const double k = __builtin_rint(x.hi * 1.4426950408889634073599);
+  // r = x − k·ln2 with k·ln2_hi exact (TwoProd)
+  const dd kh = two_prod(k, kLn2Hi);
+  dd r = dd_sub(x, kh);
+  r = dd_add_d(r, -k * kLn2Lo);
+  r = dd_ldexp(r, -9);
+  // s = e^r − 1 = r + r²/2! + … + r⁹/9!  (Horner on 1/n!)
+  constexpr double inv_fact[10] = {1.0,
+                                   1.0,
+                                   0.5,
+                                   1.6666666666666666574e-01,
+                                   4.1666666666666664354e-02,
+                                   8.3333333333333332177e-03,
+                                   1.3888888888888889419e-03,
+                                   1.9841269841269841253e-04,
+                                   2.4801587301587301566e-05,
+                                   2.7557319223985892511e-06};
+  constexpr double inv_fact_lo[10] = {0.0,
+                                      0.0,
+                                      0.0,
+                                      9.2518585385429706566e-18,
+                                      2.3129646346357426641e-18,
+                                      1.1564823173178713802e-19,
+                                      -5.3005439543735770590e-20,
+                                      1.7209558293420705286e-22,
+                                      2.1511947866775881608e-23,
+                                      -1.8583932740464720810e-22};
+  dd p = {inv_fact[9], inv_fact_lo[9]};
+#pragma unroll
+  for (int n = 8; n >= 1; --n) p = dd_add(dd_mul(p, r), dd{inv_fact[n], inv_fact_lo[n]});
+  dd s = dd_mul(p, r);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) s = dd_mul(s, dd_add_d(s, 2.0));
+  const dd e = dd_add_d(s, 1.0);
+  return dd_ldexp(e, (int)k);
+}
+
+}  // namespace yfm

@@ -45,6 +45,13 @@ struct TvlGaps {
   const int* idx = nullptr;   // device, N
 };
 hipError_t launch_tvl(const LaunchArgs& a, const TvlGaps& g, int lanes);
+// the same filter in double-double arithmetic (yfm_tvl_dd.hip): the init kernel writes the
+// per-candidate dd records into a.scratch (tvl_dd_scratch_bytes); `select` (B bytes or nullptr)
+// restricts the filter to the flagged candidates
+size_t tvl_dd_scratch_bytes(int B);
+int tvl_dd_lanes_for(int B, int N);
+hipError_t launch_tvl_dd_init(const LaunchArgs& a);
+hipError_t launch_tvl_dd(const LaunchArgs& a, const TvlGaps& g, int lanes, const unsigned char* select);
 // Trajectory outputs (yfm_predict.hip) from a recorded state trajectory.
 struct PredictArgs {
   int kind, M, L, N, P, B, T;

@@ -1,0 +1,635 @@
+// yfm_tvl_dd.hip — the TVλ extended-Kalman-filter log-likelihood carried in double-double
+// arithmetic (the "certified" precision mode, YFM_PREC_DD / YFM_PREC_AUTO of include/yfm.h).
+//
+// Restates, per candidate θ_b, exactly what yfm_tvl.hip does —
+//   get_loss                 src/models/kalman/filter.jl:182-209
+//   filter! (TVλ EKF)        src/models/kalman/filter.jl:12-80 (dZ1 = z/λ − z/(λ²m), :43)
+//   update_factor_loadings!  src/models/kalman/tvλdns.jl:53-64
+//   initialize_filter        src/models/kalman/filter.jl:1-10
+//   transform / set_params!  parameteroperations.jl:22-32, paramoperations.jl:6-68
+// — but with every quantity that feeds the state recursion (θ_c, λ, the loadings, the
+// innovation, the 14 sufficient statistics, the 4×4 capacitance solve, β and P) held as an
+// unevaluated sum of two doubles (yfm_dd.hpp).  Why: for a share of candidates the EKF's
+// own dynamics amplify a rounding by 1e10..1e13 over T = 600 steps, so any FP64 evaluation,
+// the reference's included, is up to 1e-4 from the exact value; a dd evaluation is ~1e-20
+// from it (measured against the binary128 truth, oracle/yfm_truth.c).
+// The loglik terms themselves (log|det B̃|, v'F⁻¹v) are well conditioned and are summed in
+// dd from FP64-rounded values.
+//
+// Mapping as yfm_tvl.hip: one filter per group of L lanes, lane j owning maturities
+// i ≡ j (mod L); per step each lane forms its share of the loadings and statistics, the
+// group reduces them with DPP / permlane butterflies (dd-exact pairwise sums), and every
+// lane of the group runs the 4×4 update.  Decoding and initialize_filter run in dd in
+// tvl_dd_init_kernel (one thread per candidate) and hand over a per-candidate record.
+// exp(−λ m_i) walks the maturities of a lane with the dd jump factors e^{−λ d_k}
+// (relative drift ≤ (N/L)·2^-104).
+#include "yfm_dd.hpp"
+#include "yfm_device.hpp"
+#include "yfm_internal.hpp"
+
+namespace yfm {
+
+namespace {
+
+constexpr int kDdBlock = 256;
+constexpr int kDdPre = 8;  // panel doubles prefetched per thread per chunk
+constexpr int M4 = 4;
+
+// per-candidate record written by tvl_dd_init_kernel (doubles)
+constexpr int kDSig = 0;     // σ² (dd)
+constexpr int kDDelta = 2;   // δ (4 doubles, exact θ entries)
+constexpr int kDPhi = 6;     // Φ row-major (16 dd)
+constexpr int kDQ = 38;      // Q upper triangle, row-major i ≤ k (10 dd)
+constexpr int kDBeta = 58;   // β₀ (4 dd)
+constexpr int kDP = 66;      // P₀ upper triangle (10 dd)
+constexpr int kDOk = 86;
+constexpr int kDRecLen = 88;
+constexpr int kDPar = 58;    // σ², δ, Φ, Q: the read-only part staged in LDS per group
+
+__device__ __forceinline__ int utri(int i, int k) { return i * M4 - i * (i - 1) / 2 + (k - i); }  // i ≤ k < 4
+
+// Gaussian elimination with partial pivoting (first max |hi|, the getf2 rule) on an n×n dd
+// system with R right-hand sides; false on an exact zero pivot (where getrf reports info > 0).
+template <int n, int R>
+__device__ __forceinline__ bool dd_gauss(dd (&A)[n][n], dd (&X)[n][R], dd* det_out = nullptr) {
+  bool ok = true;
+  double sgn = 1.0;
+  dd det = dd_make(1.0);
+#pragma unroll
+  for (int k = 0; k < n; ++k) {
+    int p = k;
+    double amax = fabs(A[k][k].hi);
+#pragma unroll
+    for (int i = k + 1; i < n; ++i) {
+      const double a = fabs(A[i][k].hi);
+      const bool gt = a > amax;
+      amax = gt ? a : amax;
+      p = gt ? i : p;
+    }
+    sgn = (p != k) ? -sgn : sgn;
+#pragma unroll
+    for (int i = k + 1; i < n; ++i) {
+      const bool s = (p == i);
+#pragma unroll
+      for (int c = k; c < n; ++c) {
+        const dd a = A[k][c], b = A[i][c];
+        A[k][c] = s ? b : a;
+        A[i][c] = s ? a : b;
+      }
+#pragma unroll
+      for (int c = 0; c < R; ++c) {
+        const dd a = X[k][c], b = X[i][c];
+        X[k][c] = s ? b : a;
+        X[i][c] = s ? a : b;
+      }
+    }
+    const dd piv = A[k][k];
+    ok = ok && (piv.hi != 0.0);
+    if (det_out) det = dd_mul(det, piv);
+    const dd r = dd_rcp(piv);
+#pragma unroll
+    for (int i = k + 1; i < n; ++i) {
+      const dd l = dd_mul(A[i][k], r);
+#pragma unroll
+      for (int c = k + 1; c < n; ++c) A[i][c] = dd_sub(A[i][c], dd_mul(l, A[k][c]));
+#pragma unroll
+      for (int c = 0; c < R; ++c) X[i][c] = dd_sub(X[i][c], dd_mul(l, X[k][c]));
+    }
+    A[k][k] = r;  // keep the reciprocal pivot for the back substitution
+  }
+#pragma unroll
+  for (int k = n - 1; k >= 0; --k) {
+#pragma unroll
+    for (int c = 0; c < R; ++c) {
+      dd s = X[k][c];
+#pragma unroll
+      for (int j = k + 1; j < n; ++j) s = dd_sub(s, dd_mul(A[k][j], X[j][c]));
+      X[k][c] = dd_mul(s, A[k][k]);
+    }
+  }
+  if (det_out) *det_out = sgn < 0 ? dd_neg(det) : det;
+  return ok;
+}
+
+// log of a positive dd to ~u² absolute: FP64 seed + one Newton step on e^y = x
+__device__ __forceinline__ dd dd_log(dd x) {
+  const double y0 = log(x.hi);
+  const dd e = dd_exp(dd_make(-y0));
+  const dd t = dd_add_d(dd_mul(x, e), -1.0);  // x·e^{−y0} − 1
+  return dd_add_d(t, y0);
+}
+
+// transformations.jl:21-26 as written (2y/(1+y) − 1), in dd
+__device__ __forceinline__ dd dd_from_R_to_11(double x) {
+  const dd y = dd_exp(dd_make(x));
+  if (!(y.hi < __builtin_inf())) return {__builtin_nan(""), 0.0};  // Inf/Inf
+  return dd_add_d(dd_div(dd_mul_d(y, 2.0), dd_add_d(y, 1.0)), -1.0);
+}
+
+// Sum of an unnormalised dd over the aligned group of L lanes: each butterfly level pairs
+// every lane with its partner and both form the same exact-leading-part sum, so all lanes
+// of the group end with bitwise the same value.
+template <int LVL>
+__device__ __forceinline__ void pair_exchange(double x, double& a, double& b) {
+  const int lo = __double2loint(x), hi = __double2hiint(x);
+  if constexpr (LVL <= 3) {
+    constexpr int ctrl = LVL == 0 ? 0xB1 : LVL == 1 ? 0x4E : LVL == 2 ? 0x141 : 0x140;
+    const int plo = __builtin_amdgcn_update_dpp(0, lo, ctrl, 0xf, 0xf, false);
+    const int phi = __builtin_amdgcn_update_dpp(0, hi, ctrl, 0xf, 0xf, false);
+    const double p = __hiloint2double(phi, plo);
+    // canonical order (lower lane's value first) so both partners compute the same bits
+    const bool lower = LVL == 0 ? !(threadIdx.x & 1) : LVL == 1 ? !(threadIdx.x & 2)
+                     : LVL == 2 ? !(threadIdx.x & 4) : !(threadIdx.x & 8);
+    a = lower ? x : p;
+    b = lower ? p : x;
+  } else if constexpr (LVL == 4) {
+    const auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    a = __hiloint2double(rh[0], rl[0]);
+    b = __hiloint2double(rh[1], rl[1]);
+  } else {
+    const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    a = __hiloint2double(rh[0], rl[0]);
+    b = __hiloint2double(rh[1], rl[1]);
+  }
+}
+
+template <int LVL>
+__device__ __forceinline__ void acc_level(double& hi, double& lo) {
+  double h0, h1, l0, l1;
+  pair_exchange<LVL>(hi, h0, h1);
+  pair_exchange<LVL>(lo, l0, l1);
+  const dd s = two_sum(h0, h1);
+  hi = s.hi;
+  lo = (l0 + l1) + s.lo;
+}
+
+template <int L>
+__device__ __forceinline__ dd group_sum_acc(dd_acc a) {
+  double hi = a.hi, lo = a.lo;
+  if constexpr (L >= 2) acc_level<0>(hi, lo);
+  if constexpr (L >= 4) acc_level<1>(hi, lo);
+  if constexpr (L >= 8) acc_level<2>(hi, lo);
+  if constexpr (L >= 16) acc_level<3>(hi, lo);
+  if constexpr (L >= 32) acc_level<4>(hi, lo);
+  if constexpr (L >= 64) acc_level<5>(hi, lo);
+  return two_sum(hi, lo);  // |lo| may exceed |hi| after cancellation
+}
+
+// β ← δ + Φ b;  P ← Φ X Φ'·s + Q  (X symmetric, upper triangle; s = σ² after an update, 1 for
+// the prediction-only step)
+__device__ __forceinline__ void dd_propagate(const double* par, const dd (&b)[M4], const dd (&X)[10], bool scale,
+                                             dd (&beta)[M4], dd (&P)[10]) {
+  const dd* Phi = reinterpret_cast<const dd*>(par + kDPhi);
+  const dd* Q = reinterpret_cast<const dd*>(par + kDQ);
+  const dd sig2 = *reinterpret_cast<const dd*>(par + kDSig);
+  dd A[M4][M4];
+#pragma unroll
+  for (int i = 0; i < M4; ++i) {
+    dd s = dd_make(par[kDDelta + i]);
+#pragma unroll
+    for (int j = 0; j < M4; ++j) s = dd_add(s, dd_mul(Phi[i * M4 + j], b[j]));
+    beta[i] = s;
+#pragma unroll
+    for (int j = 0; j < M4; ++j) {
+      dd_acc a;
+#pragma unroll
+      for (int l = 0; l < M4; ++l) a.add_prod(Phi[i * M4 + l], X[l <= j ? utri(l, j) : utri(j, l)]);
+      A[i][j] = a.value();
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < M4; ++i)
+#pragma unroll
+    for (int k = i; k < M4; ++k) {
+      dd_acc a;
+#pragma unroll
+      for (int l = 0; l < M4; ++l) a.add_prod(A[i][l], Phi[k * M4 + l]);
+      dd s = a.value();
+      if (scale) s = dd_mul(s, sig2);
+      P[utri(i, k)] = dd_add(s, Q[utri(i, k)]);
+    }
+}
+
+}  // namespace
+
+// decode θ_b in dd (transform_params + set_params!) and run initialize_filter (filter.jl:1-10)
+__global__ __launch_bounds__(64) void tvl_dd_init_kernel(const double* __restrict__ theta, int P, int B, int space,
+                                                         double* __restrict__ rec) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const double* th = theta + (size_t)b * P;
+  double* r = rec + (size_t)b * kDRecLen;
+  int k = 0;
+  const dd sig2 = space == 0 ? dd_exp(dd_make(th[k])) : dd_make(th[k]);
+  ++k;
+  dd U[M4][M4];
+#pragma unroll
+  for (int j = 0; j < M4; ++j)
+#pragma unroll
+    for (int i = 0; i < M4; ++i) {
+      if (i <= j) {
+        const double x = th[k++];
+        U[i][j] = (i == j && space == 0) ? dd_exp(dd_make(x)) : dd_make(x);
+      } else {
+        U[i][j] = dd_make(0.0);
+      }
+    }
+  dd Q[M4][M4];
+#pragma unroll
+  for (int i = 0; i < M4; ++i)
+#pragma unroll
+    for (int j = 0; j < M4; ++j) {
+      dd_acc a;
+#pragma unroll
+      for (int l = 0; l < M4; ++l) a.add_prod(U[l][i], U[l][j]);  // Q = U'U
+      Q[i][j] = a.value();
+    }
+  double delta[M4];
+#pragma unroll
+  for (int i = 0; i < M4; ++i) delta[i] = th[k++];
+  dd Phi[M4][M4];
+#pragma unroll
+  for (int i = 0; i < M4; ++i)
+#pragma unroll
+    for (int j = 0; j < M4; ++j) {
+      const double x = th[k++];
+      Phi[i][j] = (i == j && space == 0) ? dd_from_R_to_11(x) : dd_make(x);
+    }
+  // β₀ = (I − Φ) \ δ
+  dd A[M4][M4], x[M4][1];
+#pragma unroll
+  for (int i = 0; i < M4; ++i) {
+#pragma unroll
+    for (int j = 0; j < M4; ++j) A[i][j] = (i == j) ? dd_add_d(dd_neg(Phi[i][j]), 1.0) : dd_neg(Phi[i][j]);
+    x[i][0] = dd_make(delta[i]);
+  }
+  bool ok = dd_gauss<M4, 1>(A, x);
+  // P₀: the 10 unknowns P_ij (i ≤ j) of P − ΦPΦ' = Q (singular iff I − Φ⊗Φ is)
+  constexpr int S = 10;
+  dd Ls[S][S], qv[S][1];
+  int rr = 0;
+#pragma unroll
+  for (int i = 0; i < M4; ++i)
+#pragma unroll
+    for (int j = i; j < M4; ++j) {
+      int c = 0;
+#pragma unroll
+      for (int kk = 0; kk < M4; ++kk)
+#pragma unroll
+        for (int l = kk; l < M4; ++l) {
+          dd s = dd_mul(Phi[i][kk], Phi[j][l]);
+          if (kk != l) s = dd_add(s, dd_mul(Phi[i][l], Phi[j][kk]));
+          Ls[rr][c] = (rr == c) ? dd_add_d(dd_neg(s), 1.0) : dd_neg(s);
+          ++c;
+        }
+      qv[rr][0] = Q[i][j];
+      ++rr;
+    }
+  ok = dd_gauss<S, 1>(Ls, qv) && ok;
+  r[kDSig] = sig2.hi;
+  r[kDSig + 1] = sig2.lo;
+  int q = 0;
+#pragma unroll
+  for (int i = 0; i < M4; ++i) {
+    r[kDDelta + i] = delta[i];
+    r[kDBeta + 2 * i] = x[i][0].hi;
+    r[kDBeta + 2 * i + 1] = x[i][0].lo;
+#pragma unroll
+    for (int j = 0; j < M4; ++j) {
+      r[kDPhi + 2 * (i * M4 + j)] = Phi[i][j].hi;
+      r[kDPhi + 2 * (i * M4 + j) + 1] = Phi[i][j].lo;
+    }
+#pragma unroll
+    for (int j = i; j < M4; ++j, ++q) {
+      r[kDQ + 2 * q] = Q[i][j].hi;
+      r[kDQ + 2 * q + 1] = Q[i][j].lo;
+      r[kDP + 2 * q] = qv[q][0].hi;
+      r[kDP + 2 * q + 1] = qv[q][0].lo;
+    }
+  }
+  r[kDOk] = ok ? 1.0 : 0.0;
+  r[kDOk + 1] = 0.0;
+}
+
+template <int L, bool RECORD>
+__global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
+    const double* __restrict__ rec, int B, const double* __restrict__ Y, const double* __restrict__ prep, int ldp,
+    int np, int T, int N, int TC, const double* __restrict__ mats, int K, const double* __restrict__ gap_d,
+    const int* __restrict__ gap_idx, const int* __restrict__ T_use, const unsigned char* __restrict__ select,
+    double* __restrict__ out, unsigned int* __restrict__ flags, double* __restrict__ rec_beta,
+    double* __restrict__ rec_P, int horizon, int rec_len) {
+  constexpr int GPB = kDdBlock / L;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double* s_m = smem;                                  // m_i
+  dd* s_rm = reinterpret_cast<dd*>(smem + N);          // 1/m_i (dd)
+  double* s_nan = smem + 3 * N;                        // TC NaN flags of the staged chunk
+  double* s_y = s_nan + TC;                            // TC columns of N yields
+  double* s_par = s_y + TC * N;                        // per group: σ², δ, Φ, Q (kDPar doubles)
+  dd* s_w = reinterpret_cast<dd*>(s_par + GPB * kDPar);  // per group: e^{-λ d_k}, k < K
+  int* s_gi = reinterpret_cast<int*>(s_w + GPB * kTvlGaps);
+  __shared__ double s_gd[kTvlGaps];
+  __shared__ int s_nobs_max;
+
+  const int tid = threadIdx.x;
+  const int j = tid % L;
+  const int grp = tid / L;
+  const int b = blockIdx.x * GPB + grp;
+  // `select` (optional): evaluate only the flagged candidates (AUTO mode); others idle
+  const bool live = b < B && (!select || select[b]);
+  const int bb = b < B ? b : (B - 1);
+  const int nobs = T_use ? T_use[bb] : T;
+
+  if (tid == 0) s_nobs_max = 0;
+  for (int i = tid; i < N; i += kDdBlock) {
+    const double m = mats[i];
+    s_m[i] = m;
+    s_rm[i] = dd_rcp(dd_make(m));
+    if (K > 0) s_gi[i] = gap_idx[i];
+  }
+  if (tid < K) s_gd[tid] = gap_d[tid];
+  const double* r = rec + (size_t)bb * kDRecLen;
+  double* par = s_par + grp * kDPar;
+  for (int q = j; q < kDPar; q += L) par[q] = r[q];
+  __syncthreads();
+  const int my_steps = horizon > 0 ? nobs + horizon : nobs - 1;
+  const int my_data = horizon > 0 ? nobs : nobs - 1;
+  atomicMax(&s_nobs_max, live ? my_steps : 0);
+
+  dd beta[M4], Pm[10];
+#pragma unroll
+  for (int i = 0; i < M4; ++i) beta[i] = {r[kDBeta + 2 * i], r[kDBeta + 2 * i + 1]};
+#pragma unroll
+  for (int q = 0; q < 10; ++q) Pm[q] = {r[kDP + 2 * q], r[kDP + 2 * q + 1]};
+  const bool init_ok = r[kDOk] != 0.0;
+  const dd sig2 = {par[kDSig], par[kDSig + 1]};
+  const dd rsig2 = dd_rcp(sig2);
+
+  dd_acc sum_ld, sum_q;
+  bool neg = false;
+  double last_ld = -__builtin_inf(), last_q = 0.0;  // fresh model: F = 0 (logdet −Inf), v = 0
+  bool last_neg = false;
+
+  __syncthreads();
+  const int nsteps = max(s_nobs_max, 0);
+  const int CHY = TC * N;
+
+  double pre[kDdPre];
+  double pre_nan = 0.0;
+  auto load_chunk = [&](int c) {
+    const size_t base = (size_t)c * CHY;
+    const size_t lim = (size_t)T * N;
+#pragma unroll
+    for (int q = 0; q < kDdPre; ++q) {
+      const int e = q * kDdBlock + tid;
+      const size_t g = base + e;
+      pre[q] = (e < CHY && g < lim) ? Y[g] : 0.0;
+    }
+    const int tc = c * TC + tid;
+    pre_nan = (tid < TC && tc < T) ? prep[(size_t)tc * ldp + np + 2] : 0.0;
+  };
+  auto store_chunk = [&]() {
+#pragma unroll
+    for (int q = 0; q < kDdPre; ++q) {
+      const int e = q * kDdBlock + tid;
+      if (e < CHY) s_y[e] = pre[q];
+    }
+    if (tid < TC) s_nan[tid] = pre_nan;
+  };
+  if (nsteps > 0) {
+    load_chunk(0);
+    store_chunk();
+    __syncthreads();
+    load_chunk(1);
+  }
+
+  for (int t = 0; t < nsteps; ++t) {
+    const int tt = t % TC;
+    const bool act = live && t < my_steps;
+    const bool acc = t >= 1;  // Julia t > 1 (filter.jl:194)
+    const bool nan_col = s_nan[tt] != 0.0 || t >= my_data;
+    if (act && nan_col) {
+      // filter.jl:13-29: prediction only; F, F⁻¹, v stale → the loglik re-adds the last term
+      dd bf[M4], X[10];
+#pragma unroll
+      for (int i = 0; i < M4; ++i) bf[i] = beta[i];
+#pragma unroll
+      for (int q = 0; q < 10; ++q) X[q] = Pm[q];
+      dd_propagate(par, bf, X, false, beta, Pm);
+      if (acc) {
+        sum_ld.add(dd_make(last_ld));
+        sum_q.add(dd_make(last_q));
+        neg = neg || last_neg;
+      }
+    } else if (act) {
+      // ---- λ and the per-step constants of the loadings (tvλdns.jl:56, filter.jl:38-46) ----
+      const dd e4 = dd_exp(beta[3]);
+      const dd lam = dd_add_d(e4, 1e-2);
+      const dd dl = dd_add_d(lam, -1e-2);
+      const dd rl = dd_rcp(lam);
+      const dd c1 = dd_mul(dd_add(beta[1], beta[2]), dl);
+      const dd c2 = dd_mul(beta[2], dl);
+      const dd k1 = dd_mul(c1, rl);
+      const double* col = s_y + tt * N;
+      dd_acc S2, S3, S4, G22, G23, G24, G33, G34, G44, U1, U2, U3, U4, VV;
+      auto accum = [&](int i, dd z) {
+        const double m = s_m[i];
+        const dd it = dd_mul(rl, s_rm[i]);                // 1/τ
+        const dd z2 = dd_mul(dd_add_d(dd_neg(z), 1.0), it);  // (1 − z)/τ
+        const dd z3 = dd_sub(z2, z);
+        // ((β2+β3)(z/λ − z/(λ²m)) + β3·m·z)·(λ − 0.01) = z·(k1(1 − 1/τ·…) …): z·(k1(1 − it) + c2·m)
+        const dd z4 = dd_mul(z, dd_add(dd_mul(k1, dd_add_d(dd_neg(it), 1.0)), dd_mul_d(c2, m)));
+        const dd yh = dd_add(dd_add(beta[0], dd_mul(beta[1], z2)), dd_mul(beta[2], z3));
+        const dd v = dd_add_d(dd_neg(yh), col[i]);  // y − Z[:,1:3]β[1:3]
+        S2.add(z2);
+        S3.add(z3);
+        S4.add(z4);
+        G22.add_prod(z2, z2);
+        G23.add_prod(z2, z3);
+        G24.add_prod(z2, z4);
+        G33.add_prod(z3, z3);
+        G34.add_prod(z3, z4);
+        G44.add_prod(z4, z4);
+        U1.add(v);
+        U2.add_prod(z2, v);
+        U3.add_prod(z3, v);
+        U4.add_prod(z4, v);
+        VV.add_prod(v, v);
+      };
+      if (K > 0) {
+        dd* w = s_w + grp * kTvlGaps;
+        for (int q = j; q < K; q += L) w[q] = dd_exp(dd_neg(dd_mul_d(lam, s_gd[q])));
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        dd z = (j < N) ? dd_exp(dd_neg(dd_mul_d(lam, s_m[j]))) : dd_make(0.0);
+        for (int i = j; i < N; i += L) {
+          const dd wn = w[s_gi[i]];
+          accum(i, z);
+          z = dd_mul(z, wn);
+        }
+      } else {
+        for (int i = j; i < N; i += L) accum(i, dd_exp(dd_neg(dd_mul_d(lam, s_m[i]))));
+      }
+      dd G[M4][M4];
+      G[0][0] = dd_make((double)N);
+      G[0][1] = G[1][0] = group_sum_acc<L>(S2);
+      G[0][2] = G[2][0] = group_sum_acc<L>(S3);
+      G[0][3] = G[3][0] = group_sum_acc<L>(S4);
+      G[1][1] = group_sum_acc<L>(G22);
+      G[1][2] = G[2][1] = group_sum_acc<L>(G23);
+      G[1][3] = G[3][1] = group_sum_acc<L>(G24);
+      G[2][2] = group_sum_acc<L>(G33);
+      G[2][3] = G[3][2] = group_sum_acc<L>(G34);
+      G[3][3] = group_sum_acc<L>(G44);
+      const dd u[M4] = {group_sum_acc<L>(U1), group_sum_acc<L>(U2), group_sum_acc<L>(U3), group_sum_acc<L>(U4)};
+      const dd vv = group_sum_acc<L>(VV);
+
+      // ---- capacitance solve: B̃ = σ²I + P G, W = B̃⁻¹P ----
+      dd A[M4][M4], W[M4][M4];
+#pragma unroll
+      for (int i = 0; i < M4; ++i)
+#pragma unroll
+        for (int c = 0; c < M4; ++c) {
+          dd_acc a;
+          if (i == c) a.add(sig2);
+#pragma unroll
+          for (int l = 0; l < M4; ++l) a.add_prod(Pm[i <= l ? utri(i, l) : utri(l, i)], G[l][c]);
+          A[i][c] = a.value();
+          W[i][c] = Pm[i <= c ? utri(i, c) : utri(c, i)];
+        }
+      dd det;
+      dd_gauss<M4, M4>(A, W, &det);
+      dd Ws[10];
+#pragma unroll
+      for (int i = 0; i < M4; ++i)
+#pragma unroll
+        for (int c = i; c < M4; ++c) Ws[utri(i, c)] = (i == c) ? W[i][i] : dd_ldexp(dd_add(W[i][c], W[c][i]), -1);
+      dd bf[M4];
+      dd_acc uk;
+#pragma unroll
+      for (int i = 0; i < M4; ++i) {
+        dd_acc a;
+#pragma unroll
+        for (int c = 0; c < M4; ++c) a.add_prod(Ws[i <= c ? utri(i, c) : utri(c, i)], u[c]);
+        const dd kv = a.value();
+        bf[i] = dd_add(beta[i], kv);
+        uk.add_prod(u[i], kv);
+      }
+      const double q = dd_to_double(dd_mul(dd_sub(vv, uk.value()), rsig2));
+      const double dh = dd_to_double(det);
+      const bool upd = dh != 0.0;  // inv(F) threw: return without updating (filter.jl:51-56)
+      if (upd) dd_propagate(par, bf, Ws, true, beta, Pm);
+      last_ld = upd ? log(fabs(dh)) : -__builtin_inf();
+      last_q = upd ? q : __builtin_nan("");
+      last_neg = dh < 0.0;
+      if (acc) {
+        sum_ld.add(dd_make(last_ld));
+        sum_q.add(dd_make(last_q));
+        neg = neg || last_neg;
+      }
+    }
+    if constexpr (RECORD) {
+      const int slot = t - max(0, my_steps - rec_len);
+      if (act && j == 0 && slot >= 0) {
+        const size_t o = (size_t)b * (size_t)rec_len + slot;
+#pragma unroll
+        for (int i = 0; i < M4; ++i) rec_beta[o * M4 + i] = dd_to_double(beta[i]);
+        if (rec_P) {
+#pragma unroll
+          for (int c = 0; c < M4; ++c)
+#pragma unroll
+            for (int i = 0; i < M4; ++i) rec_P[o * M4 * M4 + c * M4 + i] = dd_to_double(Pm[i <= c ? utri(i, c) : utri(c, i)]);
+        }
+      }
+    }
+    if (tt == TC - 1) {
+      __syncthreads();
+      store_chunk();
+      __syncthreads();
+      load_chunk(t / TC + 2);
+    }
+  }
+
+  if (!live || j != 0) return;
+  double ll;
+  if (!init_ok) {
+    ll = __builtin_nan("");
+    atomicAdd(&flags[0], 1u);
+  } else {
+    const int nterms = max(nobs - 2, 0);
+    if (nterms == 0) {
+      ll = 0.0;
+    } else {
+      // per term: (N − 4)·log σ² + N·log 2π (+ log|det B̃_t| + q_t, summed above)
+      const dd lsig = dd_log(sig2);
+      dd tot = dd_mul_d(dd_add_d(dd_mul_d(lsig, (double)(N - M4)), (double)N * kLog2Pi), (double)nterms);
+      tot = dd_add(tot, dd_add(sum_ld.value(), sum_q.value()));
+      ll = -0.5 * dd_to_double(tot);
+    }
+    if (neg || !isfinite(ll)) {
+      ll = -__builtin_inf();
+      atomicAdd(&flags[1], 1u);
+    }
+  }
+  out[b] = ll;
+}
+
+namespace {
+
+template <int L>
+hipError_t launch_tvl_dd_l(const LaunchArgs& a, const TvlGaps& g, int TC, const unsigned char* select) {
+  constexpr int GPB = kDdBlock / L;
+  const int grid = (a.B + GPB - 1) / GPB;
+  const size_t shmem = sizeof(double) * (size_t)(3 * a.N + TC + TC * a.N + GPB * kDPar + 2 * GPB * kTvlGaps) +
+                       sizeof(int) * a.N;
+  if (a.rec_beta) {
+    hipLaunchKernelGGL((tvl_dd_loglik_kernel<L, true>), dim3(grid), dim3(kDdBlock), shmem, a.stream, a.scratch, a.B,
+                       a.raw, a.panel, a.ldp, a.np, a.T, a.N, TC, a.mats, g.K, g.d, g.idx, a.T_use, select, a.out,
+                       a.flags, a.rec_beta, a.rec_P, a.horizon, a.rec_len);
+  } else {
+    hipLaunchKernelGGL((tvl_dd_loglik_kernel<L, false>), dim3(grid), dim3(kDdBlock), shmem, a.stream, a.scratch, a.B,
+                       a.raw, a.panel, a.ldp, a.np, a.T, a.N, TC, a.mats, g.K, g.d, g.idx, a.T_use, select, a.out,
+                       a.flags, nullptr, nullptr, 0, 0);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace
+
+size_t tvl_dd_scratch_bytes(int B) { return sizeof(double) * (size_t)kDRecLen * (size_t)(B > 0 ? B : 1); }
+
+int tvl_dd_lanes_for(int B, int N) {
+  // one wave per SIMD of lanes (the kernel needs the whole 512-register file per lane)
+  long long want = (1024LL * 64 + B - 1) / (B > 0 ? B : 1);
+  int L = 1;
+  while (L < want && L < 64) L <<= 1;
+  int capN = 1;
+  while (capN < N && capN < 64) capN <<= 1;
+  return L < capN ? L : capN;
+}
+
+hipError_t launch_tvl_dd_init(const LaunchArgs& a) {
+  hipLaunchKernelGGL(tvl_dd_init_kernel, dim3((a.B + 63) / 64), dim3(64), 0, a.stream, a.theta, a.P, a.B, a.space,
+                     a.scratch);
+  return hipGetLastError();
+}
+
+hipError_t launch_tvl_dd(const LaunchArgs& a, const TvlGaps& g, int lanes, const unsigned char* select) {
+  int TC = (kDdPre * kDdBlock) / a.N;
+  if (TC > 32) TC = 32;
+  if (TC < 1) return hipErrorInvalidValue;
+  switch (lanes) {
+    case 1: return launch_tvl_dd_l<1>(a, g, TC, select);
+    case 2: return launch_tvl_dd_l<2>(a, g, TC, select);
+    case 4: return launch_tvl_dd_l<4>(a, g, TC, select);
+    case 8: return launch_tvl_dd_l<8>(a, g, TC, select);
+    case 16: return launch_tvl_dd_l<16>(a, g, TC, select);
+    case 32: return launch_tvl_dd_l<32>(a, g, TC, select);
+    case 64: return launch_tvl_dd_l<64>(a, g, TC, select);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace yfm

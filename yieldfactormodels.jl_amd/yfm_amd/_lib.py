@@ -40,11 +40,16 @@ SIGNATURES = {
                                     _D]),
     "yfm_estimate": (ctypes.c_int, [_V, ctypes.c_int, ctypes.c_int, _D, ctypes.c_int, ctypes.c_int, _I, ctypes.c_int,
                                     ctypes.c_double, ctypes.c_int, ctypes.c_double, _D, _D, _D, _I, _LL]),
+    "yfm_set_precision": (ctypes.c_int, [_V, ctypes.c_int]),
+    "yfm_get_precision": (ctypes.c_int, [_V]),
     "yfm_loss_array": (ctypes.c_int, [_V, ctypes.c_int, ctypes.c_int, _D, ctypes.c_int, ctypes.c_int, _I, ctypes.c_int,
                                       _D]),
 }
 
-ABI_VERSION = 1
+ABI_VERSION = 2
+
+# precision modes (include/yfm.h: enum yfm_precision)
+PREC_FP64, PREC_DD, PREC_AUTO = 0, 1, 2
 
 
 class YFMError(RuntimeError):

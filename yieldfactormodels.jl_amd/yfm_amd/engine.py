@@ -39,6 +39,15 @@ class Engine:
         except Exception:
             pass
 
+    # ---- precision (TVλ arithmetic, include/yfm.h: yfm_set_precision) -----------------
+    @property
+    def precision(self) -> int:
+        return self.lib.yfm_get_precision(self.ctx)
+
+    @precision.setter
+    def precision(self, mode: int) -> None:
+        _lib.check(self.lib.yfm_set_precision(self.ctx, int(mode)))
+
     # ---- panel -------------------------------------------------------------------
     def set_panel(self, data, maturities, force: bool = False):
         """data: N×T (maturities × months) like the reference's ``data`` matrix."""
