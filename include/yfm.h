@@ -58,16 +58,15 @@ enum yfm_status {
   YFM_EUNSUPPORTED = -4 /* valid request this build has no kernel for */
 };
 
-/* precision — arithmetic of the TVλ EKF (the fixed-loading models always run FP64: their
- * filter is contracting and the collapsed form is within 1e-12 of exact arithmetic)
- *   YFM_PREC_FP64  FP64 throughout (the reference's own arithmetic class; fastest).
- *   YFM_PREC_DD    double-double (~106-bit) recursion: for candidates whose EKF amplifies
- *                  rounding by 1e10..1e13 (no FP64 evaluation, the reference's included, is
- *                  then within 1e-9 of the exact value) the result stays ~1e-20 from it.
- *   YFM_PREC_AUTO  FP64, then a second FP64 evaluation with a different summation order and
- *                  initialisation rounding; candidates whose two values differ by more than
- *                  1e-13 relative are re-evaluated in double-double. */
-enum yfm_precision { YFM_PREC_FP64 = 0, YFM_PREC_DD = 1, YFM_PREC_AUTO = 2 };
+/* precision — the arithmetic of the TVλ EKF (the fixed-loading models always run FP64: their
+ * filter contracts, and the collapsed form stays within 1e-12 of exact arithmetic)
+ *   YFM_PREC_CERTIFIED (default)  TVλ in double-double (~106-bit) arithmetic.  A share of TVλ
+ *       candidates amplify any FP64 rounding by 1e10..1e13 over T = 600 steps, so no FP64
+ *       evaluation — the reference's own dense path included — is then within 1e-9 of the
+ *       exact value of filter.jl:12-80; this mode returns that value to the last FP64 bit
+ *       (checked against a binary128 restatement).  ≈7× the cost of FP64.
+ *   YFM_PREC_FP64  FP64 throughout: the reference's arithmetic class and the fastest path. */
+enum yfm_precision { YFM_PREC_CERTIFIED = 0, YFM_PREC_FP64 = 1 };
 
 /* Library/ABI introspection. */
 int yfm_abi_version(void);
@@ -83,7 +82,7 @@ const char* yfm_last_error(void);
 yfm_ctx* yfm_create(int hip_device);
 void yfm_destroy(yfm_ctx* ctx);
 
-/* Select the TVλ arithmetic for subsequent calls on this context (default YFM_PREC_FP64).
+/* Select the TVλ arithmetic for subsequent calls on this context (default YFM_PREC_CERTIFIED).
  * The reference has no such switch: its Float64 path is YFM_PREC_FP64's arithmetic class. */
 int yfm_set_precision(yfm_ctx* ctx, int precision);
 int yfm_get_precision(yfm_ctx* ctx);

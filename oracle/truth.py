@@ -71,3 +71,13 @@ def states_truth(kind, Y, mats, theta, space=0):
                                               th.ctypes.data_as(_D), beta.ctypes.data_as(_D), P.ctypes.data_as(_D),
                                               ctypes.byref(ll))
     return ll.value, beta, P
+
+
+def predict_states_truth(kind, Y, mats, theta, horizon=1, space=1):
+    """State trajectory of predict (filter.jl:250-282) on hcat(Y, NaN × (horizon − 1)) in binary128:
+    A (T + horizon, M), A[j] = β after filter! step j + 1 (the final NaN step included) — the
+    layout of kalman_ld.predict_traj_tvl for one candidate."""
+    Y = np.asarray(Y, dtype=np.float64)
+    pad = np.hstack([Y, np.full((Y.shape[0], horizon + 1), np.nan)])
+    _, beta, _ = states_truth(kind, pad, mats, theta, space)
+    return beta.T

@@ -1,8 +1,8 @@
 """GPU parity of the fixed-loading models at maturity counts beyond the per-lane kernel
 (N > 64 → yfm_group.hip: one filter per lane group, DPP reductions), e.g. the 360 monthly
 maturities of config 3's panel — vs the NumPy oracle (dense N×N LAPACK path) and the C oracle.
-Tolerance: the parity rule of test_gpu_parity.assert_parity (1e-9 relative, adjudicated by the
-long-double truth proxy where the dense oracle is itself further than that from exact
+Tolerance: the parity rule of test_gpu_parity.assert_parity (1e-9 relative, adjudicated at
+factor 1 by the binary128 truth where the dense oracle is itself further than that from exact
 arithmetic), normwise on the state trajectories."""
 from __future__ import annotations
 
@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 from oracle import kalman_oracle as O
-from oracle.kalman_ld import loglik_ld
+from oracle.truth import loglik_truth
 from test_gpu_parity import assert_ll_close, assert_parity
 from yfm_amd import KIND_DNS, KIND_GNS
 from yfm_amd import synthetic as S
@@ -29,9 +29,9 @@ def test_large_n_loglik_vs_oracle(engine, kind, N, T):
     got = engine.loglik(kind, Th)
     ref = np.array([O.loglik(kind, mats, state_dim(kind), Y, Th[:, b]) for b in range(12)])
     # the dense N×N FP64 oracle can itself be ~1e-9 from exact arithmetic at N = 360: the
-    # long-double proxy adjudicates (assert_parity: within 1e-9 of the oracle, or closer to the
-    # truth than the oracle is)
-    assert_parity(got, ref, loglik_ld(kind, mats, Y, Th))
+    # binary128 truth adjudicates (assert_parity: within 1e-9 of the oracle, or at least as close
+    # to the truth as the oracle is)
+    assert_parity(got, ref, loglik_truth(kind, Y, mats, Th))
 
 
 def test_large_n_windows_nan_states_and_predict(engine):

@@ -1,121 +1,147 @@
-"""GPU parity of the TVλ extended Kalman filter kernel (yfm_tvl.hip) — SURVEY §8 a8, config 3.
+"""GPU parity of the TVλ extended Kalman filter (yfm_tvl_dd.hip / yfm_tvl.hip) — SURVEY §8 a8, config 3.
 
-Oracles: the committed golden fixture (NumPy restatement, tests/golden/tvl_basic.npz, with
-a 40-digit truth for its first candidate) and the independent C restatement
-(oracle/yfm_oracle.c: dense N×N getrf+getri per step, the reference's algorithm) at the
-config-3 cross-section N = 360.  Tolerance: 1e-9 relative on the loglik (north star).
+Oracles: the C restatement of the reference's dense path (oracle/yfm_oracle.c: F = ZPZ' + σ²I
+formed, getrf + getri and a logdet LU every step — filter.jl:12-80, :182-209) and the binary128
+evaluation of the same recursion (oracle/yfm_truth.c, pinned to the 40-digit dense mpmath
+restatement in tests/test_oracle.py).
+
+Rule (north star, factor 1, no noise-floor allowance): within 1e-9 relative of the oracle, or at
+least as close to the truth as the oracle is.  The default precision (YFM_PREC_CERTIFIED, the
+double-double filter) must meet it on every candidate and is additionally checked to reproduce
+the truth to ~1e-13.  YFM_PREC_FP64 is the reference's arithmetic class: on candidates whose EKF
+amplifies rounding (config 3: a quarter of the batch) no FP64 evaluation — the oracle's included
+— is within 1e-9 of exact arithmetic, so for it the tests assert reproducibility and report the
+(within 1e-9, adjudicated, failing) table.
 """
 from __future__ import annotations
 
-import ctypes
 import os
 
 import numpy as np
 import pytest
 
-from conftest import ROOT, load_golden
-from oracle.kalman_ld import loglik_ld_tvl
-from test_gpu_parity import REL, assert_ll_close, assert_parity
+from conftest import GOLDEN, load_golden
+from oracle.truth import loglik_oracle, loglik_truth, states_truth
+from test_gpu_parity import assert_parity, parity_table
 from yfm_amd import KIND_TVL
+from yfm_amd import _lib
 from yfm_amd import synthetic as S
 
 pytestmark = pytest.mark.gpu
 
-LANES = [1, 2, 4, 8, 16, 32, 64]
+EXACT = 1e-13  # the certified filter vs binary128 truth (measured: 0 on the config-3 sample)
 
 
-def engine_default_lanes(B):
-    """The launcher's own choice (yfm_tvl.hip: tvl_lanes_for) for N = 360."""
-    L = 1
-    while L < min(64, -(-131072 // B)):
-        L *= 2
-    return L
+class env:
+    """Set environment overrides of the TVλ launcher (read per call): YFM_TVL_LANES, YFM_TVL_EXP."""
 
-
-class lanes_override:
-    """Force the lanes-per-filter choice of the TVλ launcher (YFM_TVL_LANES, read per call)."""
-
-    def __init__(self, L):
-        self.L = L
+    def __init__(self, **kv):
+        self.kv = {k: str(v) for k, v in kv.items()}
 
     def __enter__(self):
-        os.environ["YFM_TVL_LANES"] = str(self.L)
+        os.environ.update(self.kv)
 
     def __exit__(self, *exc):
-        os.environ.pop("YFM_TVL_LANES", None)
+        for k in self.kv:
+            os.environ.pop(k, None)
 
 
-def c_oracle(Y, mats, Th, T_use=None, threads=16):
-    lib = ctypes.CDLL(str(ROOT / "oracle" / "libyfm_oracle.so"))
-    D = ctypes.POINTER(ctypes.c_double)
-    Yf = np.asfortranarray(Y)
-    Thf = np.asfortranarray(Th)
-    N, T = Yf.shape
-    P, B = Thf.shape
-    out = np.empty(B)
-    tu = None
-    if T_use is not None:
-        tu = np.ascontiguousarray(T_use, dtype=np.int32)
-    lib.yfm_oracle_loglik(KIND_TVL, 0, Yf.ctypes.data_as(D), N, T, np.ascontiguousarray(mats).ctypes.data_as(D),
-                          Thf.ctypes.data_as(D), P, B,
-                          None if tu is None else tu.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
-                          out.ctypes.data_as(D), threads)
-    return out
+class precision:
+    def __init__(self, engine, mode):
+        self.engine, self.mode = engine, mode
+
+    def __enter__(self):
+        self.old = self.engine.precision
+        self.engine.precision = self.mode
+
+    def __exit__(self, *exc):
+        self.engine.precision = self.old
 
 
-@pytest.mark.parametrize("L", LANES)
-def test_tvl_golden_every_group_width(engine, L):
+def rel(a, b):
+    fin = np.isfinite(b)
+    return np.abs(a[fin] - b[fin]) / np.maximum(np.abs(b[fin]), 1e-300)
+
+
+def test_default_precision_is_certified(engine):
+    assert engine.precision == _lib.PREC_CERTIFIED
+
+
+@pytest.mark.parametrize("L", [4, 8, 16, 32, 64])
+def test_tvl_golden_certified_every_group_width(engine, L):
     g = load_golden("tvl_basic")
+    truth = loglik_truth(KIND_TVL, g["Y"], g["maturities"], g["Theta"])
     engine.set_panel(g["Y"], g["maturities"])
-    with lanes_override(L):
+    with env(YFM_TVL_LANES=L):
         got = engine.loglik(KIND_TVL, g["Theta"])
-    k = len(g["ll_truth"])
-    assert_parity(got[:k], g["loglik"][:k], g["ll_truth"])
-    assert_ll_close(got[k:], g["loglik"][k:])
+    assert_parity(got, g["loglik"], truth)
+    assert rel(got, truth).max() <= EXACT
 
 
-@pytest.mark.parametrize("L", [1, 8, 64])
-def test_tvl_states_vs_truth(engine, L):
+@pytest.mark.parametrize("L", [1, 2, 4, 8, 16, 32, 64])
+def test_tvl_golden_fp64_every_group_width(engine, L):
+    g = load_golden("tvl_basic")
+    truth = loglik_truth(KIND_TVL, g["Y"], g["maturities"], g["Theta"])
+    engine.set_panel(g["Y"], g["maturities"])
+    with precision(engine, _lib.PREC_FP64), env(YFM_TVL_LANES=L):
+        got = engine.loglik(KIND_TVL, g["Theta"])
+    assert_parity(got, g["loglik"], truth)
+
+
+@pytest.mark.parametrize("mode", [_lib.PREC_CERTIFIED, _lib.PREC_FP64])
+def test_tvl_states_vs_truth(engine, mode):
+    """β and P after every filter! call (filter.jl:12-80) vs the binary128 trajectories."""
     g = load_golden("tvl_basic")
     engine.set_panel(g["Y"], g["maturities"])
-    with lanes_override(L):
-        ll, beta, P = engine.filter_states(KIND_TVL, g["Theta"][:, :1])
-    for got, ora, tru in ((beta[..., 0], g["beta_traj"][..., 0], g["beta_truth"][..., 0]),
-                          (P[..., 0], g["P_traj"][..., 0], g["P_truth"][..., 0])):
-        scale = np.abs(tru).max()
-        oracle_err = np.abs(ora - tru).max() / scale
-        assert np.abs(got - ora).max() / scale <= max(REL, 2 * oracle_err)
-        assert np.abs(got - tru).max() / scale <= 1e-10
+    with precision(engine, mode):
+        ll, beta, P = engine.filter_states(KIND_TVL, g["Theta"][:, :2])
+    for b in range(2):
+        _, bt, Pt = states_truth(KIND_TVL, g["Y"], g["maturities"], g["Theta"][:, b], space=int(g["space"]))
+        tol = EXACT if mode == _lib.PREC_CERTIFIED else 1e-10
+        for got, tru in ((beta[..., b], bt), (P[..., b], Pt)):
+            assert np.abs(got - tru).max() / np.abs(tru).max() <= tol
 
 
 @pytest.fixture(scope="module")
 def config3():
     mats = S.maturities_360()
     Y = S.simulate_panel(KIND_TVL, 600, maturities=mats)
-    return Y, mats
+    with np.load(GOLDEN / "config3" / "tvl_config3_sample.npz", allow_pickle=False) as z:
+        fx = {k: z[k] for k in z.files}
+    return Y, mats, fx
 
 
-def test_tvl_config3_cross_section_vs_c_oracle(engine, config3):
-    """N = 360 maturities (config 3), T = 100, 32 candidates: the C restatement of the reference's dense
-    360×360 path vs the kernel at its default group width and at L = 1 / 64."""
-    Y, mats = config3
-    Y = np.asfortranarray(Y[:, :100])
-    Th = S.theta_batch(KIND_TVL, 32, seed=31, bad_frac=0.0, scale=0.02)
-    Th[:, 0] = S.theta0(KIND_TVL)
-    ref = c_oracle(Y, mats, Th)
-    truth = loglik_ld_tvl(mats, Y, Th)
-    alt = loglik_ld_tvl(mats, Y, Th, dtype=np.float64)
+def test_tvl_config3_sample_certified(engine, config3):
+    """Config 3's workload (N = 360, T = 600) on the first 64 candidates of the bench batch: every
+    candidate within 1e-9 of the dense oracle or at least as close to the binary128 truth (factor
+    1) — where the oracle itself is up to 3e-4 from exact arithmetic."""
+    Y, mats, fx = config3
     engine.set_panel(Y, mats)
-    got = engine.loglik(KIND_TVL, Th)
-    assert_parity(got, ref, truth, alt=alt)
-    for L in (1, 64):
-        with lanes_override(L):
-            assert_parity(engine.loglik(KIND_TVL, Th), ref, truth, alt=alt)
+    got = engine.loglik(KIND_TVL, fx["Theta"])
+    table = assert_parity(got, fx["loglik_oracle"], fx["loglik_truth"])
+    print("certified", table)
+    assert table["failing"] == 0 and table["within_1e-9"] + table["adjudicated"] == 64
+    assert rel(got, fx["loglik_truth"]).max() <= EXACT
+
+
+def test_tvl_config3_sample_fp64(engine, config3):
+    """The FP64 filter on the same sample: bitwise reproducible, the oracle's −Inf / NaN pattern,
+    and at least as accurate as the reference's dense FP64 path in the median; the (within 1e-9,
+    adjudicated, failing) table is printed."""
+    Y, mats, fx = config3
+    engine.set_panel(Y, mats)
+    with precision(engine, _lib.PREC_FP64):
+        got = engine.loglik(KIND_TVL, fx["Theta"])
+        np.testing.assert_array_equal(engine.loglik(KIND_TVL, fx["Theta"]), got)
+    ora, tru = fx["loglik_oracle"], fx["loglik_truth"]
+    assert np.array_equal(np.isfinite(got), np.isfinite(ora)) and np.array_equal(np.isnan(got), np.isnan(ora))
+    print("fp64", parity_table(got, ora, tru))
+    assert np.median(rel(got, tru)) <= max(np.median(rel(ora, tru)), 1e-13)
 
 
 def test_tvl_windows_nan_and_edges(engine, config3):
     """T_use windows, NaN columns (prediction-only steps, stale F/v re-added), tiny T."""
-    Y, mats = config3
+    Y, mats, _ = config3
     sub = np.arange(0, 360, 9)  # N = 40
     Yn = np.asfortranarray(Y[sub, :90].copy())
     Yn[:, [5, 6, 50]] = np.nan
@@ -123,22 +149,26 @@ def test_tvl_windows_nan_and_edges(engine, config3):
     m = mats[sub].copy()
     Th = S.theta_batch(KIND_TVL, 12, seed=37, bad_frac=0.0, scale=0.02)
     tu = np.array([1, 2, 3, 10, 40, 89, 90, 90, 64, 65, 33, 77], dtype=np.int32)
-    ref = c_oracle(Yn, m, Th, T_use=tu)
-    truth = loglik_ld_tvl(m, Yn, Th, T_use=tu)
-    alt = loglik_ld_tvl(m, Yn, Th, T_use=tu, dtype=np.float64)
+    ref = loglik_oracle(KIND_TVL, Yn, m, Th, T_use=tu)
+    truth = loglik_truth(KIND_TVL, Yn, m, Th, T_use=tu)
     engine.set_panel(Yn, m)
-    for L in (1, 4, 64):
-        with lanes_override(L):
-            assert_parity(engine.loglik(KIND_TVL, Th, T_use=tu), ref, truth, alt=alt)
+    for L in (4, 64):
+        with env(YFM_TVL_LANES=L):
+            got = engine.loglik(KIND_TVL, Th, T_use=tu)
+        assert_parity(got, ref, truth)
+        assert rel(got, truth).max(initial=0.0) <= EXACT
+    with precision(engine, _lib.PREC_FP64):
+        for L in (1, 4, 64):
+            with env(YFM_TVL_LANES=L):
+                got = engine.loglik(KIND_TVL, Th, T_use=tu)
+            assert np.array_equal(np.isfinite(got), np.isfinite(ref)) and np.array_equal(np.isnan(got), np.isnan(ref))
 
 
 def test_tvl_full_batch_properties(engine, config3):
-    """Config 3 at B = 16,384, T = 600, N = 360: deterministic, independent of batch position, flags
-    consistent; and independent of the group width up to rounding: on 48 candidates the default width
-    and L = 64 are each within max(1e-9, 100 × the error of an FP64 NumPy run of the same algebra) of the
-    long-double truth (the TVλ EKF is ill-conditioned for a sizeable share of candidates: FP64 rounding
-    alone moves their loglik by 1e-8..1e-3, for the reference's dense path even more — DESIGN.md §5)."""
-    Y, mats = config3
+    """Config 3 at B = 16,384, T = 600, N = 360 in the default precision: deterministic, independent
+    of batch position, flag counters consistent, exact (vs binary128) on a 48-candidate sample;
+    the FP64 mode has the same −Inf / NaN pattern."""
+    Y, mats, _ = config3
     engine.set_panel(Y, mats)
     Th = S.theta_batch(KIND_TVL, 16384, seed=41, bad_frac=0.01, scale=0.02)
     a = engine.loglik(KIND_TVL, Th)
@@ -146,43 +176,46 @@ def test_tvl_full_batch_properties(engine, config3):
     assert n_throw == np.isnan(a).sum() and n_neginf == np.isneginf(a).sum()
     np.testing.assert_array_equal(engine.loglik(KIND_TVL, Th), a)
     perm = np.random.default_rng(5).permutation(16384)[:512]
-    with lanes_override(engine_default_lanes(16384)):
+    with env(YFM_TVL_LANES=4):  # the launcher's width at B = 16,384
         c = engine.loglik(KIND_TVL, np.asfortranarray(Th[:, perm]))
     np.testing.assert_array_equal(c, a[perm])  # same group width → bitwise position independent
     assert np.isfinite(a).mean() > 0.9
     sub = np.asfortranarray(Th[:, perm[:48]])
-    truth = loglik_ld_tvl(mats, Y, sub)
-    fp64 = loglik_ld_tvl(mats, Y, sub, dtype=np.float64)
-    with lanes_override(64):
-        w64 = engine.loglik(KIND_TVL, sub)
-    fin = np.isfinite(truth)
-    assert np.array_equal(fin, np.isfinite(a[perm[:48]])) and np.array_equal(fin, np.isfinite(w64))
-    bound = np.maximum(1e-9, 100 * np.abs(fp64[fin] - truth[fin]) / np.abs(truth[fin]))
-    for got in (a[perm[:48]], w64):
-        assert np.all(np.abs(got[fin] - truth[fin]) / np.abs(truth[fin]) <= bound)
+    truth = loglik_truth(KIND_TVL, Y, mats, sub)
+    assert np.array_equal(np.isfinite(truth), np.isfinite(a[perm[:48]]))
+    assert rel(a[perm[:48]], truth).max() <= EXACT
+    with precision(engine, _lib.PREC_FP64):
+        f = engine.loglik(KIND_TVL, Th)
+    assert np.array_equal(np.isfinite(f), np.isfinite(a)) and np.array_equal(np.isnan(f), np.isnan(a))
 
 
 @pytest.mark.parametrize("grid", ["wu30", "irregular"])
 def test_tvl_maturity_grids_and_exp_paths(engine, grid):
     """The exp recurrence over maturity jumps (≤ 8 distinct m_{i+L} − m_i) vs one exp per maturity
-    (YFM_TVL_EXP=1, also the automatic fallback for irregular grids), against the C oracle + truth."""
+    (YFM_TVL_EXP=1, also the automatic fallback for irregular grids), both precisions."""
     if grid == "wu30":
         mats = S.maturities_30()
     else:
         mats = np.sort(np.random.default_rng(3).uniform(1.0, 360.0, 24)).round(3)
     Y = S.simulate_panel(KIND_TVL, 80, maturities=mats)
     Th = S.theta_batch(KIND_TVL, 16, seed=43, bad_frac=0.0, scale=0.02)
-    ref = c_oracle(Y, mats, Th)
-    truth = loglik_ld_tvl(mats, Y, Th)
-    alt = loglik_ld_tvl(mats, Y, Th, dtype=np.float64)
+    ref = loglik_oracle(KIND_TVL, Y, mats, Th)
+    truth = loglik_truth(KIND_TVL, Y, mats, Th)
     engine.set_panel(Y, mats)
-    for L in (1, 4, 16):
-        with lanes_override(L):
+    for L in (4, 16):
+        with env(YFM_TVL_LANES=L):
             rec = engine.loglik(KIND_TVL, Th)
-            os.environ["YFM_TVL_EXP"] = "1"
-            try:
+            with env(YFM_TVL_EXP=1):
                 ex = engine.loglik(KIND_TVL, Th)
-            finally:
-                os.environ.pop("YFM_TVL_EXP", None)
-        assert_parity(rec, ref, truth, alt=alt)
-        assert_parity(ex, ref, truth, alt=alt)
+        for got in (rec, ex):
+            assert_parity(got, ref, truth)
+            assert rel(got, truth).max() <= EXACT
+    with precision(engine, _lib.PREC_FP64):
+        for L in (1, 4, 16):
+            with env(YFM_TVL_LANES=L):
+                rec = engine.loglik(KIND_TVL, Th)
+                with env(YFM_TVL_EXP=1):
+                    ex = engine.loglik(KIND_TVL, Th)
+            for got in (rec, ex):
+                assert np.array_equal(np.isfinite(got), np.isfinite(ref))
+                print(grid, L, parity_table(got, ref, truth))

@@ -71,7 +71,7 @@ struct DevBuf {
 
 struct yfm_ctx {
   int device = 0;
-  int precision = YFM_PREC_FP64;  // TVλ arithmetic (yfm_set_precision)
+  int precision = YFM_PREC_CERTIFIED;  // TVλ arithmetic (yfm_set_precision)
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;  // θ uploads of pipelined host-pointer batches (created lazily)
   // panel
@@ -81,12 +81,14 @@ struct yfm_ctx {
   DevBuf theta, out, tuse, rec_beta, rec_P;
   DevBuf flags;  // 4 × unsigned int: n_init_throw, n_neg_inf, deferred-candidate count, pad
   DevBuf scratch;  // per-candidate work records (TVλ init)
+  DevBuf scratch_dd;  // TVλ double-double records (YFM_PREC_CERTIFIED)
   DevBuf traj, init_bad;       // trajectory-mode state records, per-candidate init-throw marks
   DevBuf defer;                // list of candidates handed from the per-lane to the group kernel
   DevBuf tiled_raw, tiled_panel;  // get_loss_array with K > 1 passes: the panel tiled K times
   // TVλ maturity-jump tables, one per lane count L = 2^l (built lazily, reset by set_panel)
   std::vector<double> mats_host;
   int gap_K[7] = {-1, -1, -1, -1, -1, -1, -1};
+  bool gap_exact[7] = {};
   DevBuf gap_buf[7];
 };
 
@@ -132,8 +134,13 @@ int tvl_gaps(yfm_ctx* ctx, int L, yfm::TvlGaps& g) {
     std::vector<double> d;
     std::vector<int> idx(N, 0);
     bool ok = true;
+    bool exact = true;
     for (int i = 0; i + L < N && ok; ++i) {
-      const double gap = ctx->mats_host[i + L] - ctx->mats_host[i];
+      const double hi = ctx->mats_host[i + L], lo = ctx->mats_host[i];
+      const double gap = hi - lo;
+      // TwoSum error of the subtraction: the double-double filter needs the jumps exactly
+      const double bb = gap - hi;
+      exact = exact && ((hi - (gap - bb)) + (-lo - bb)) == 0.0;
       int k = 0;
       while (k < (int)d.size() && d[k] != gap) ++k;
       if (k == (int)d.size()) {
@@ -153,8 +160,10 @@ int tvl_gaps(yfm_ctx* ctx, int L, yfm::TvlGaps& g) {
                               hipMemcpyHostToDevice));
     }
     ctx->gap_K[l] = K;
+    ctx->gap_exact[l] = exact;
   }
   g.K = ctx->gap_K[l];
+  g.exact = ctx->gap_exact[l];
   if (g.K > 0) {
     char* base = static_cast<char*>(ctx->gap_buf[l].p);
     g.d = reinterpret_cast<const double*>(base);
@@ -216,18 +225,17 @@ int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int 
       const int l = std::atoi(ov);
       if (l >= 1 && l <= 64 && (l & (l - 1)) == 0) lanes = l;
     }
-    if (ctx->precision == YFM_PREC_DD) {
-      if (!std::getenv("YFM_TVL_LANES")) lanes = yfm::tvl_dd_lanes_for(B, ctx->N);
-      YFM_HIP_CHECK(ctx->scratch.ensure(yfm::tvl_dd_scratch_bytes(B)));
-      a.scratch = static_cast<double*>(ctx->scratch.p);
-      yfm::TvlGaps g;
+    yfm::TvlGaps g;
+    if (ctx->precision == YFM_PREC_CERTIFIED) {
+      lanes = yfm::tvl_dd_lanes_for(B, ctx->N, std::getenv("YFM_TVL_LANES") ? lanes : 0);
+      YFM_HIP_CHECK(ctx->scratch_dd.ensure(yfm::tvl_dd_scratch_bytes(B)));
+      double* rdd = static_cast<double*>(ctx->scratch_dd.p);
       if (int r = tvl_gaps(ctx, lanes, g)) return r;
-      e = yfm::launch_tvl_dd_init(a);
-      if (e == hipSuccess) e = yfm::launch_tvl_dd(a, g, lanes, nullptr);
+      e = yfm::launch_tvl_dd_init(a, rdd);
+      if (e == hipSuccess) e = yfm::launch_tvl_dd(a, rdd, g, lanes);
     } else {
       YFM_HIP_CHECK(ctx->scratch.ensure(yfm::tvl_scratch_bytes(B)));
       a.scratch = static_cast<double*>(ctx->scratch.p);
-      yfm::TvlGaps g;
       if (int r = tvl_gaps(ctx, lanes, g)) return r;
       e = yfm::launch_tvl(a, g, lanes);
     }
@@ -362,6 +370,7 @@ void yfm_destroy(yfm_ctx* ctx) {
                     &ctx->rec_P, &ctx->flags, &ctx->scratch})
     b->release();
   for (DevBuf* b : {&ctx->traj, &ctx->init_bad, &ctx->tiled_raw, &ctx->tiled_panel, &ctx->defer}) b->release();
+  ctx->scratch_dd.release();
   for (DevBuf& b : ctx->gap_buf) b.release();
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
@@ -370,7 +379,7 @@ void yfm_destroy(yfm_ctx* ctx) {
 
 int yfm_set_precision(yfm_ctx* ctx, int precision) {
   if (int r = check_ctx(ctx)) return r;
-  if (precision != YFM_PREC_FP64 && precision != YFM_PREC_DD && precision != YFM_PREC_AUTO)
+  if (precision != YFM_PREC_CERTIFIED && precision != YFM_PREC_FP64)
     return set_error(YFM_EINVAL, "unknown precision %d", precision);
   ctx->precision = precision;
   return YFM_OK;

@@ -41,17 +41,21 @@ size_t tvl_scratch_bytes(int B);
 constexpr int kTvlGaps = 8;
 struct TvlGaps {
   int K = 0;
+  bool exact = false;         // every jump is the exact difference of its two maturities
   const double* d = nullptr;  // device, kTvlGaps
   const int* idx = nullptr;   // device, N
 };
 hipError_t launch_tvl(const LaunchArgs& a, const TvlGaps& g, int lanes);
-// the same filter in double-double arithmetic (yfm_tvl_dd.hip): the init kernel writes the
-// per-candidate dd records into a.scratch (tvl_dd_scratch_bytes); `select` (B bytes or nullptr)
-// restricts the filter to the flagged candidates
+// per-candidate FP64 record of the TVλ init kernel (decoded θ + initial state), doubles
+constexpr int kRecSigma = 0, kRecDelta = 1, kRecPhi = 5, kRecQ = 21, kRecBeta = 31, kRecP = 35, kRecOk = 45;
+constexpr int kRecLen = 48;  // padded to 16-byte multiples
+// the same filter in double-double arithmetic (yfm_tvl_dd.hip), YFM_PREC_CERTIFIED: the init
+// kernel writes the per-candidate dd records into `rec_dd` (tvl_dd_scratch_bytes(B));
+// tvl_dd_lanes_for picks the lanes per filter (`want` > 0: a requested width, clamped)
 size_t tvl_dd_scratch_bytes(int B);
-int tvl_dd_lanes_for(int B, int N);
-hipError_t launch_tvl_dd_init(const LaunchArgs& a);
-hipError_t launch_tvl_dd(const LaunchArgs& a, const TvlGaps& g, int lanes, const unsigned char* select);
+int tvl_dd_lanes_for(int B, int N, int want);
+hipError_t launch_tvl_dd_init(const LaunchArgs& a, double* rec_dd);
+hipError_t launch_tvl_dd(const LaunchArgs& a, const double* rec_dd, const TvlGaps& g, int lanes);
 // Trajectory outputs (yfm_predict.hip) from a recorded state trajectory.
 struct PredictArgs {
   int kind, M, L, N, P, B, T;

@@ -46,10 +46,9 @@ constexpr int kTvlPre = 8;  // panel doubles prefetched per thread per chunk (â‰
 // loadings are nearly collinear (measured: 1.8e-8 on a random N = 33, T = 3 case).
 enum : int { S2 = 0, S3, S4, G22, G23, G24, G33, G34, G44, U1, U2, U3, U4, VV, NSTAT };
 
-// Per-candidate record written by tvl_init_kernel: the decoded parameters and the
-// initial state, so the filter kernel never holds the 10Ã—10 Lyapunov system in VGPRs.
-constexpr int kRecSigma = 0, kRecDelta = 1, kRecPhi = 5, kRecQ = 21, kRecBeta = 31, kRecP = 35, kRecOk = 45;
-constexpr int kRecLen = 48;  // doubles (padded to 16-byte multiples)
+// Per-candidate record written by tvl_init_kernel (layout kRec* in yfm_internal.hpp): the
+// decoded parameters and the initial state, so the filter kernel never holds the 10Ã—10
+// Lyapunov system in VGPRs.
 
 // decode Î¸_b (transform_params + set_params!) and run initialize_filter (filter.jl:1-10)
 __global__ __launch_bounds__(256) void tvl_init_kernel(const double* __restrict__ theta, int P, int B, int space,

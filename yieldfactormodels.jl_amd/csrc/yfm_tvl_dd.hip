@@ -1,5 +1,5 @@
 // yfm_tvl_dd.hip — the TVλ extended-Kalman-filter log-likelihood carried in double-double
-// arithmetic (the "certified" precision mode, YFM_PREC_DD / YFM_PREC_AUTO of include/yfm.h).
+// arithmetic (the default precision mode, YFM_PREC_CERTIFIED of include/yfm.h).
 //
 // Restates, per candidate θ_b, exactly what yfm_tvl.hip does —
 //   get_loss                 src/models/kalman/filter.jl:182-209
@@ -317,8 +317,7 @@ template <int L, bool RECORD>
 __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
     const double* __restrict__ rec, int B, const double* __restrict__ Y, const double* __restrict__ prep, int ldp,
     int np, int T, int N, int TC, const double* __restrict__ mats, int K, const double* __restrict__ gap_d,
-    const int* __restrict__ gap_idx, const int* __restrict__ T_use, const unsigned char* __restrict__ select,
-    double* __restrict__ out, unsigned int* __restrict__ flags, double* __restrict__ rec_beta,
+    const int* __restrict__ gap_idx, const int* __restrict__ T_use, double* __restrict__ out, unsigned int* __restrict__ flags, double* __restrict__ rec_beta,
     double* __restrict__ rec_P, int horizon, int rec_len) {
   constexpr int GPB = kDdBlock / L;
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -336,9 +335,8 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
   const int j = tid % L;
   const int grp = tid / L;
   const int b = blockIdx.x * GPB + grp;
-  // `select` (optional): evaluate only the flagged candidates (AUTO mode); others idle
-  const bool live = b < B && (!select || select[b]);
-  const int bb = b < B ? b : (B - 1);
+  const bool live = b < B;
+  const int bb = live ? b : (B - 1);
   const int nobs = T_use ? T_use[bb] : T;
 
   if (tid == 0) s_nobs_max = 0;
@@ -579,20 +577,21 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
 namespace {
 
 template <int L>
-hipError_t launch_tvl_dd_l(const LaunchArgs& a, const TvlGaps& g, int TC, const unsigned char* select) {
+hipError_t launch_tvl_dd_l(const LaunchArgs& a, const double* rec_dd, const TvlGaps& g, int TC) {
   constexpr int GPB = kDdBlock / L;
   const int grid = (a.B + GPB - 1) / GPB;
   const size_t shmem = sizeof(double) * (size_t)(3 * a.N + TC + TC * a.N + GPB * kDPar + 2 * GPB * kTvlGaps) +
                        sizeof(int) * a.N;
-  if (a.rec_beta) {
-    hipLaunchKernelGGL((tvl_dd_loglik_kernel<L, true>), dim3(grid), dim3(kDdBlock), shmem, a.stream, a.scratch, a.B,
-                       a.raw, a.panel, a.ldp, a.np, a.T, a.N, TC, a.mats, g.K, g.d, g.idx, a.T_use, select, a.out,
-                       a.flags, a.rec_beta, a.rec_P, a.horizon, a.rec_len);
-  } else {
-    hipLaunchKernelGGL((tvl_dd_loglik_kernel<L, false>), dim3(grid), dim3(kDdBlock), shmem, a.stream, a.scratch, a.B,
-                       a.raw, a.panel, a.ldp, a.np, a.T, a.N, TC, a.mats, g.K, g.d, g.idx, a.T_use, select, a.out,
-                       a.flags, nullptr, nullptr, 0, 0);
+  if (shmem > 160 * 1024) return hipErrorInvalidValue;  // gfx950: 160 KiB of LDS per workgroup
+  auto* k = a.rec_beta ? &tvl_dd_loglik_kernel<L, true> : &tvl_dd_loglik_kernel<L, false>;
+  if (shmem > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)shmem);
+    if (e != hipSuccess) return e;
   }
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kDdBlock), shmem, a.stream, rec_dd, a.B, a.raw, a.panel, a.ldp, a.np, a.T,
+                     a.N, TC, a.mats, g.K, g.d, g.idx, a.T_use, a.out, a.flags, a.rec_beta, a.rec_P,
+                     a.rec_beta ? a.horizon : 0, a.rec_beta ? a.rec_len : 0);
   return hipGetLastError();
 }
 
@@ -600,34 +599,44 @@ hipError_t launch_tvl_dd_l(const LaunchArgs& a, const TvlGaps& g, int TC, const 
 
 size_t tvl_dd_scratch_bytes(int B) { return sizeof(double) * (size_t)kDRecLen * (size_t)(B > 0 ? B : 1); }
 
-int tvl_dd_lanes_for(int B, int N) {
-  // one wave per SIMD of lanes (the kernel needs the whole 512-register file per lane)
-  long long want = (1024LL * 64 + B - 1) / (B > 0 ? B : 1);
+int tvl_dd_lanes_for(int B, int N, int want) {
+  // one wave per SIMD of lanes (the kernel needs the whole 512-register file per lane), at
+  // least 4 lanes per filter (the per-group parameter block of 256 / L groups must fit the
+  // 64 KiB of dynamic LDS a launch gets by default), capped at the maturity count
   int L = 1;
-  while (L < want && L < 64) L <<= 1;
-  int capN = 1;
-  while (capN < N && capN < 64) capN <<= 1;
-  return L < capN ? L : capN;
+  if (want > 0) {
+    while (L < want && L < 64) L <<= 1;
+  } else {
+    const long long lanes = (1024LL * 64 + B - 1) / (B > 0 ? B : 1);
+    while (L < lanes && L < 64) L <<= 1;
+    int capN = 1;
+    while (capN < N && capN < 64) capN <<= 1;
+    L = L < capN ? L : capN;
+  }
+  return L < 4 ? 4 : L;
 }
 
-hipError_t launch_tvl_dd_init(const LaunchArgs& a) {
+hipError_t launch_tvl_dd_init(const LaunchArgs& a, double* rec_dd) {
   hipLaunchKernelGGL(tvl_dd_init_kernel, dim3((a.B + 63) / 64), dim3(64), 0, a.stream, a.theta, a.P, a.B, a.space,
-                     a.scratch);
+                     rec_dd);
   return hipGetLastError();
 }
 
-hipError_t launch_tvl_dd(const LaunchArgs& a, const TvlGaps& g, int lanes, const unsigned char* select) {
+hipError_t launch_tvl_dd(const LaunchArgs& a, const double* rec_dd, const TvlGaps& g_in, int lanes) {
+  // the recurrence z_{i+L} = z_i·e^{−λ d} is only as exact as the jumps d: a rounded maturity
+  // difference would put an FP64-sized error into every loading, so such grids take one dd exp
+  // per maturity
+  TvlGaps g = g_in;
+  if (!g.exact) g.K = 0;
   int TC = (kDdPre * kDdBlock) / a.N;
   if (TC > 32) TC = 32;
   if (TC < 1) return hipErrorInvalidValue;
   switch (lanes) {
-    case 1: return launch_tvl_dd_l<1>(a, g, TC, select);
-    case 2: return launch_tvl_dd_l<2>(a, g, TC, select);
-    case 4: return launch_tvl_dd_l<4>(a, g, TC, select);
-    case 8: return launch_tvl_dd_l<8>(a, g, TC, select);
-    case 16: return launch_tvl_dd_l<16>(a, g, TC, select);
-    case 32: return launch_tvl_dd_l<32>(a, g, TC, select);
-    case 64: return launch_tvl_dd_l<64>(a, g, TC, select);
+    case 4: return launch_tvl_dd_l<4>(a, rec_dd, g, TC);
+    case 8: return launch_tvl_dd_l<8>(a, rec_dd, g, TC);
+    case 16: return launch_tvl_dd_l<16>(a, rec_dd, g, TC);
+    case 32: return launch_tvl_dd_l<32>(a, rec_dd, g, TC);
+    case 64: return launch_tvl_dd_l<64>(a, rec_dd, g, TC);
   }
   return hipErrorInvalidValue;
 }

@@ -49,7 +49,7 @@ SIGNATURES = {
 ABI_VERSION = 2
 
 # precision modes (include/yfm.h: enum yfm_precision)
-PREC_FP64, PREC_DD, PREC_AUTO = 0, 1, 2
+PREC_CERTIFIED, PREC_FP64 = 0, 1
 
 
 class YFMError(RuntimeError):
