@@ -14,10 +14,12 @@ Other configs (same JSON contract, `config.workload` names them):
      every window's θ split evenly over the GPUs, RCCL all-gather of logliks (strong scaling)
   5  5-factor GNS extension: 1,048,576 candidates split over the GPUs, RCCL argmax (strong)
 
-Prints ONE JSON line on rank 0 with a `roofline` object (FP64 VALU bound, SURVEY §8d
-algorithmic flops ÷ HIP-event time of the launches on the library's stream) and a
-`cpu_baseline` object (the faithful dense-LU C restatement, oracle/yfm_oracle.c, on a
-bounded sample of the same workload, OpenMP over the host cores).
+Prints ONE JSON line on rank 0 with a `roofline` object (FP64 VALU bound: the algorithmic flops
+of the formulation the dominant kernel runs ÷ HIP-event time of its launches on the library's
+stream) and a `cpu_baseline` object (the faithful dense-LU C restatement, oracle/yfm_oracle.c, on
+a bounded sample of the same workload, OpenMP over the host cores; plus the optimised CPU variant
+and the binary128-adjudicated parity of the sample).  TVλ runs in the library's default certified
+(double-double) precision; `fp64_mode` reports the FP64 mode beside it.
 """
 from __future__ import annotations
 
@@ -39,25 +41,54 @@ sys.path.insert(0, str(ROOT / "yieldfactormodels.jl_amd"))
 sys.path.insert(0, str(ROOT))
 
 from yfm_amd import KIND_DNS, KIND_GNS, KIND_TVL, Engine, n_params, state_dim  # noqa: E402
+from yfm_amd import _lib  # noqa: E402
 from yfm_amd import distributed as D  # noqa: E402
 from yfm_amd import synthetic as S  # noqa: E402
 
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector, AMD spec (the local guide lists no FP64 figure)
+# v_fma_f64 microbenchmark at steady clock (tools/fp64_peak.hip, profiles/r1/fp64_peak.txt):
+# 42.9 TFLOP/s at 1 wave per SIMD, 44.7 at 2, 68.7 at 8
+FP64_MEASURED_TFLOPS = 68.7
 METRIC = "Kalman loglik evals/sec (DNS, T=600, N=30)"
 
 
+def collapsed_update_flops(M: int) -> float:
+    """FP64 operations of one collapsed-form measurement + time update at state dimension M, as
+    yfm_fixedz.hpp runs it (a division / reciprocal counts as one operation): ĉ = G⁻¹Z'y from z̃,
+    the residual ỹ'ỹ − z̃'ĉ, S = P + R, its LDLᵀ, the solves for c and the M columns of R, q,
+    β_{t|t}, P_{t|t}, β ← δ + Φβ, P ← ΦPΦ' + Q and the loglik accumulation."""
+    nz = M - 1
+    f = nz + 2 * M * nz + 2 * nz + 1          # z̃/σ², ĉ, residual, ĉ₀ += ȳ
+    f += M + M * (M + 1) // 2                 # c = ĉ − β, S = P + R (lower)
+    f += sum(2 * j + 1 + (M - 1 - j) * (2 * j + 1) for j in range(M)) + (M - 1)  # LDLᵀ + det
+    solve = 2 * M * (M - 1) + M
+    f += solve + 2 * M + 2                    # x = S⁻¹c, c'x, q
+    f += 2 * M * M                            # β_{t|t} = β + P x
+    f += M * solve + M * M * (M + 1)          # S⁻¹R column by column, P_{t|t} = P S⁻¹R
+    f += 2 * M * M + 2 * M ** 3 + M * M * (M + 1)  # β ← δ + Φβ, A = ΦP, P = AΦ' + Q
+    return f + 3
+
+
 def alg_flops_step(kind: int, N: int, M: int) -> float:
-    """SURVEY.md §8(d) algorithmic FP64 flops of one update step (capacitance/Woodbury form):
-    fixed loadings 4NM + 3N + 12⅔M³ + 6M² + 6M + 8; TVλ ≈ 62N + 939 (+ N+1 exps, not counted)."""
+    """Algorithmic FP64 flops of one update step of the formulation this build runs:
+    fixed loadings (DNS, GNS5): the collapsed form — z̃ = Z'ỹ (2N(M−1)) plus the M×M update;
+    TVλ: the capacitance form of SURVEY.md §8(d), 62N + 939 (+ N+1 exps, not counted)."""
+    if kind == KIND_TVL:
+        return 62.0 * N + 939.0
+    return 2.0 * N * (M - 1) + collapsed_update_flops(M)
+
+
+def survey_flops_step(kind: int, N: int, M: int) -> float:
+    """SURVEY.md §8(d)'s per-step count (capacitance/Woodbury form): 4NM + 3N + 12⅔M³ + 6M² + 6M + 8."""
     if kind == KIND_TVL:
         return 62.0 * N + 939.0
     return 4 * N * M + 3 * N + (38.0 / 3.0) * M ** 3 + 6 * M * M + 6 * M + 8
 
 
-def alg_flops(kind: int, N: int, M: int, T) -> np.ndarray:
-    """Per-eval algorithmic flops for window lengths T (scalar or array): (T-1)·F_step + 2NM² + 2(M²)³."""
+def alg_flops(kind: int, N: int, M: int, T, step=alg_flops_step) -> np.ndarray:
+    """Per-eval flops for window lengths T (scalar or array): (T-1)·F_step + 2NM² + 2(M²)³ (init)."""
     T = np.asarray(T, dtype=np.float64)
-    return (T - 1) * alg_flops_step(kind, N, M) + 2 * N * M * M + 2 * (M * M) ** 3
+    return (T - 1) * step(kind, N, M) + 2 * N * M * M + 2 * (M * M) ** 3
 
 
 @dataclass
@@ -113,65 +144,118 @@ def make_workload(config: int, world: int, rank: int, T: int, batch: int | None)
     raise ValueError(config)
 
 
-def cpu_baseline(w: Workload, seconds: float, gpu_out: np.ndarray):
-    """Faithful reference-path restatement on the host: time a bounded sample of the same workload."""
-    lib = ctypes.CDLL(str(ROOT / "oracle" / "libyfm_oracle.so"))
+def _host_cpu() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _native_libs():
+    """The dense port and the optimised variant built with -march=native for THIS host (the in-tree
+    builds target x86-64-v3 so they load anywhere); falls back to the in-tree builds."""
+    import subprocess
+    import tempfile
+    out = Path(tempfile.mkdtemp(prefix="yfm_cpu_"))
+    try:
+        subprocess.run(["make", "-C", str(ROOT / "oracle"), "-s", "native", f"OUT={out}"], check=True,
+                       capture_output=True, timeout=120)
+        return (ctypes.CDLL(str(out / "libyfm_oracle_native.so")), ctypes.CDLL(str(out / "libyfm_cpu_fast_native.so")),
+                "-O3 -march=native")
+    except Exception:  # noqa: BLE001
+        return (ctypes.CDLL(str(ROOT / "oracle" / "libyfm_oracle.so")),
+                ctypes.CDLL(str(ROOT / "oracle" / "libyfm_cpu_fast.so")), "-O3 -march=x86-64-v3 (native build failed)")
+
+
+def _timed(fn, w: Workload, order, chunk, threads, seconds, min_chunks=1):
+    """Evaluate the sample w.Theta[:, order] chunk by chunk with fn(…) until `seconds` have passed;
+    returns (evals/s, evaluated count, logliks)."""
     Dp = ctypes.POINTER(ctypes.c_double)
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     Yf = np.asfortranarray(w.Y)
     N, T = Yf.shape
     P = w.Theta.shape[0]
-    # sample order: the batch as laid out, except for windows (config 4), where a seeded permutation
-    # keeps the sample's mix of window lengths equal to the workload's
-    order = np.arange(w.Theta.shape[1]) if w.T_use is None else np.random.default_rng(0).permutation(w.Theta.shape[1])
-    done, t0 = 0, time.perf_counter()
-    chunk = threads if w.kind == KIND_TVL else 2 * threads
-    res = []
-    while time.perf_counter() - t0 < seconds and done + chunk <= w.Theta.shape[1]:
+    done, res, t0 = 0, [], time.perf_counter()
+    while (time.perf_counter() - t0 < seconds or len(res) < min_chunks) and done + chunk <= len(order):
         sel = order[done:done + chunk]
         sub = np.asfortranarray(w.Theta[:, sel])
         out = np.empty(chunk)
-        tu = None
-        if w.T_use is not None:
-            tu = np.ascontiguousarray(w.T_use[sel], dtype=np.int32)
-        lib.yfm_oracle_loglik(w.kind, 0, Yf.ctypes.data_as(Dp), N, T, w.mats.ctypes.data_as(Dp), sub.ctypes.data_as(Dp),
-                              P, chunk, None if tu is None else tu.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
-                              out.ctypes.data_as(Dp), threads)
+        tu = None if w.T_use is None else np.ascontiguousarray(w.T_use[sel], dtype=np.int32)
+        fn(w.kind, 0, Yf.ctypes.data_as(Dp), N, T, w.mats.ctypes.data_as(Dp), sub.ctypes.data_as(Dp), P, chunk,
+           None if tu is None else tu.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), out.ctypes.data_as(Dp), threads)
         res.append(out)
         done += chunk
     dt = time.perf_counter() - t0
-    ref = np.concatenate(res) if res else np.zeros(0)
-    got = gpu_out[order[:done]]
-    fin = np.isfinite(ref)
-    same_pattern = bool(np.array_equal(np.isfinite(got), fin) and np.array_equal(np.isnan(got), np.isnan(ref)))
-    err = np.abs(got[fin] - ref[fin]) / np.maximum(np.abs(ref[fin]), 1e-300)
-    parity = {"pattern_match": same_pattern, "gpu_vs_oracle_max_rel": float(err.max()) if err.size else 0.0,
-              "frac_within_1e-9": float((err <= 1e-9).mean()) if err.size else 1.0}
-    if w.kind in (KIND_DNS, KIND_GNS) and w.T_use is None:
-        # adjudicate with the extended-precision truth proxy on the first 512 of the sample
-        from oracle.kalman_ld import loglik_ld
-        k = min(512, done)
-        tru = loglik_ld(w.kind, w.mats, w.Y, w.Theta[:, :k])
-        ft = np.isfinite(tru)
-        e_gpu = np.abs(got[:k][ft] - tru[ft]) / np.abs(tru[ft])
-        e_ref = np.abs(ref[:k][ft] - tru[ft]) / np.abs(tru[ft])
-        parity.update(truth_subset=k, gpu_vs_truth_max_rel=float(e_gpu.max()) if e_gpu.size else 0.0,
-                      oracle_vs_truth_max_rel=float(e_ref.max()) if e_ref.size else 0.0)
+    return (done / dt if dt > 0 else 0.0), done, (np.concatenate(res) if res else np.zeros(0))
+
+
+def cpu_baseline(w: Workload, seconds: float, gpu_out: np.ndarray):
+    """CPU paths on the host cores, each on a bounded sample of the same workload:
+      value                  — the faithful restatement of the reference (oracle/yfm_oracle.c: N×N
+                               getrf+getri + logdet LU every step), OpenMP over the host threads;
+      dense_batch_1_thread   — the same on a threads×64 batch at 1 thread (BASELINE.md protocol);
+      single_theta_1_thread  — config 1: one θ, one thread;
+      optimised              — the CPU counterpart of the GPU algorithm (oracle/yfm_cpu_fast.c:
+                               collapsed form, 8 candidates per vector; TVλ capacitance form), at
+                               the host threads and at 1 thread — NOT the reference's algorithm;
+      parity                 — GPU vs the dense oracle on the sample, adjudicated by the binary128
+                               truth (oracle/yfm_truth.c): (within 1e-9, adjudicated, failing)."""
+    from oracle.truth import loglik_truth
+    dense, fast, flags = _native_libs()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
+    B = w.Theta.shape[1]
+    # sample order: the batch as laid out, except for windows (config 4), where a seeded permutation
+    # keeps the sample's mix of window lengths equal to the workload's
+    order = np.arange(B) if w.T_use is None else np.random.default_rng(0).permutation(B)
+    tvl = w.kind == KIND_TVL
+    rate, done, ref = _timed(dense.yfm_oracle_loglik, w, order, threads if tvl else 2 * threads, threads, seconds)
+    N, T = w.Y.shape
     win = "" if w.T_use is None else " with the workload's window lengths"
-    # config 1 (BASELINE.json configs[0]): one θ, single thread — the reference's own CPU case
+    out = {"value": rate, "unit": "evals/s", "cores": threads, "kind": "port", "host_cpu": _host_cpu(),
+           "sample": f"{done} of the benchmark's θ (T={T}, N={N}){win}, dense N×N getrf+getri + logdet LU per step "
+                     f"(oracle/yfm_oracle.c, {flags}, OpenMP {threads} threads)"}
+    # BASELINE.md: a threads×64 batch at 1 thread (bounded: TVλ evals take seconds each)
+    r1, n1, _ = _timed(dense.yfm_oracle_loglik, w, order, 1, 1, min(seconds, 8.0), min_chunks=3)
+    out["dense_batch_1_thread"] = {"evals_per_s": r1, "evals_timed": n1, "batch": threads * 64,
+                                   "note": "bounded by time; the full batch would take "
+                                           f"{threads * 64 / max(r1, 1e-12):.0f} s"}
     th0 = np.asfortranarray(w.Theta[:, :1])
-    one = np.empty(1)
-    n1, t1 = 0, time.perf_counter()
-    while n1 < 3 or (time.perf_counter() - t1 < 2.0 and n1 < 200):
-        lib.yfm_oracle_loglik(w.kind, 0, Yf.ctypes.data_as(Dp), N, T, w.mats.ctypes.data_as(Dp), th0.ctypes.data_as(Dp),
-                              P, 1, None, one.ctypes.data_as(Dp), 1)
-        n1 += 1
-    ms1 = 1e3 * (time.perf_counter() - t1) / n1
-    return {"value": done / dt if dt > 0 else 0.0, "unit": "evals/s", "cores": threads, "kind": "port",
-            "sample": f"{done} of the benchmark's θ (T={T}, N={N}){win} in {dt:.1f} s, dense N×N getrf+getri + "
-                      f"logdet LU per step (oracle/yfm_oracle.c, -O3, OpenMP {threads} threads)",
-            "single_theta_1_thread": {"ms_per_eval": ms1, "evals_per_s": 1e3 / ms1, "evals_timed": n1},
-            "parity": parity}
+    w1 = Workload(w.config, w.kind, w.label, w.mats, w.Y, th0, None, 1, w.scaling, False)
+    r0, n0, _ = _timed(dense.yfm_oracle_loglik, w1, np.zeros(200, dtype=np.int64), 1, 1, 2.0, min_chunks=3)
+    out["single_theta_1_thread"] = {"ms_per_eval": 1e3 / r0, "evals_per_s": r0, "evals_timed": n0}
+    ro, no, _ = _timed(fast.yfm_cpu_fast_loglik, w, order, 64 * threads if not tvl else 4 * threads, threads,
+                       min(seconds, 5.0), min_chunks=2)
+    ro1, no1, _ = _timed(fast.yfm_cpu_fast_loglik, w, order, 64 if not tvl else 4, 1, min(seconds, 3.0), min_chunks=2)
+    out["optimised"] = {"evals_per_s": ro, "evals_timed": no, "cores": threads, "evals_per_s_1_thread": ro1,
+                        "evals_timed_1_thread": no1,
+                        "kind": "optimised CPU variant, NOT the reference algorithm: "
+                                + ("capacitance form, one candidate per thread" if tvl else
+                                   "collapsed form of DESIGN.md §3.1, 8 candidates per SIMD vector")
+                                + f" (oracle/yfm_cpu_fast.c, {flags})"}
+    # parity on the dense sample, adjudicated by the binary128 truth
+    k = min(done, 64 if tvl else 512)
+    sel = order[:k]
+    got = gpu_out[sel]
+    tru = loglik_truth(w.kind, w.Y, w.mats, w.Theta[:, sel], T_use=None if w.T_use is None else w.T_use[sel],
+                       nthreads=threads)
+    o = ref[:k]
+    pat = bool(np.array_equal(np.isfinite(got), np.isfinite(o)) and np.array_equal(np.isnan(got), np.isnan(o)))
+    fin = np.isfinite(o) & np.isfinite(got)
+    e_go = np.abs(got[fin] - o[fin]) / np.maximum(np.abs(o[fin]), 1e-300)
+    e_gt = np.abs(got[fin] - tru[fin]) / np.maximum(np.abs(tru[fin]), 1e-300)
+    e_ot = np.abs(o[fin] - tru[fin]) / np.maximum(np.abs(tru[fin]), 1e-300)
+    within = e_go <= 1e-9
+    adj = ~within & (e_gt <= e_ot)
+    e_all = np.abs(gpu_out[order[:done]] - ref) / np.maximum(np.abs(ref), 1e-300)
+    out["parity"] = {"pattern_match": pat, "sample": int(k), "within_1e-9": int(within.sum()),
+                     "adjudicated": int(adj.sum()), "failing": int((~within & ~adj).sum()),
+                     "gpu_vs_truth_max_rel": float(e_gt.max()) if e_gt.size else 0.0,
+                     "oracle_vs_truth_max_rel": float(e_ot.max()) if e_ot.size else 0.0,
+                     "frac_within_1e-9_whole_sample": float(np.mean(e_all[np.isfinite(ref)] <= 1e-9)) if done else 1.0,
+                     "rule": "within 1e-9 of the dense oracle, or |gpu − truth| ≤ |oracle − truth| (binary128 truth)"}
+    return out
 
 
 def pmc_executed_flops(kernel_substr: str):
@@ -198,8 +282,38 @@ def pmc_traffic(kernel_substr: str):
     return None, None
 
 
-DOMINANT = {KIND_DNS: "fixedz_loglik_kernel<30, 3, 1, false>", KIND_TVL: "tvl_loglik_kernel",
-            KIND_GNS: "fixedz_loglik_kernel<30, 5, 2, false>"}
+DOMINANT = {KIND_DNS: "fixedz_loglik_kernel<30, 3, 1, false>", KIND_GNS: "fixedz_loglik_kernel<30, 5, 2, false>",
+            (KIND_TVL, "fp64"): "tvl_loglik_kernel", (KIND_TVL, "certified"): "tvl_dd_loglik_kernel"}
+
+
+def roofline(kind, prec, N, M, T, T_use, B, P, kernel_ms):
+    """The dominant kernel against the FP64 VALU roofline: achieved = algorithmic flops of the
+    formulation it runs (alg_flops) for this GPU's batch ÷ HIP-event time per launch."""
+    Tb = T_use if T_use is not None else np.full(B, T)
+    f_rank = float(np.sum(alg_flops(kind, N, M, Tb)))
+    f_survey = float(np.sum(alg_flops(kind, N, M, Tb, survey_flops_step)))
+    achieved = f_rank / (kernel_ms * 1e-3) / 1e12
+    name = DOMINANT[(kind, prec)] if kind == KIND_TVL else DOMINANT[kind]
+    traffic, traffic_src = pmc_traffic(name)
+    exe = pmc_executed_flops(name)
+    steps = float(np.sum(Tb - 1))
+    exe_tf = exe * steps / (kernel_ms * 1e-3) / 1e12 if exe else None
+    return {"bound": "fp64-valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": achieved / FP64_PEAK_TFLOPS, "frac_vs_measured_peak": achieved / FP64_MEASURED_TFLOPS,
+            "measured_peak": FP64_MEASURED_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
+            "algorithmic_bytes": B * (P + 1) * 8 + T * (N + 4) * 8, "kernel": name, "kernel_ms": kernel_ms,
+            "flops_per_eval": f_rank / max(B, 1),
+            "flop_model": ("SURVEY §8d capacitance form (62N + 939 per step)" if kind == KIND_TVL else
+                           "collapsed form: 2N(M−1) for Z'ỹ + the M×M update (bench.py collapsed_update_flops)"),
+            "survey_equiv_tflops": f_survey / (kernel_ms * 1e-3) / 1e12,
+            "executed_tflops": exe_tf, "executed_frac": exe_tf / FP64_PEAK_TFLOPS if exe_tf else None,
+            "executed_frac_vs_measured_peak": exe_tf / FP64_MEASURED_TFLOPS if exe_tf else None,
+            "note": "kernel_ms = HIP events around each library call in the timed region, on its stream "
+                    "(TVλ: init + filter kernels); executed_* = PMC-counted FP64 flops of the same kernel "
+                    "(profiles/); peak = AMD spec, measured_peak = v_fma_f64 microbenchmark at 8 waves/SIMD"
+                    + ("; certified precision runs the same algorithm in double-double (≈7× the FP64 "
+                       "instructions), frac is of the algorithm's FP64 count" if kind == KIND_TVL and prec == "certified"
+                       else "")}
 
 
 def main():
@@ -210,6 +324,8 @@ def main():
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
     ap.add_argument("--batch", type=int, default=None, help="θ per GPU (2, 3), per window (4), total (5)")
     ap.add_argument("--T", type=int, default=600)
+    ap.add_argument("--precision", choices=["certified", "fp64"], default="certified",
+                    help="TVλ arithmetic (include/yfm.h yfm_set_precision; the library default is certified)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -231,6 +347,8 @@ def main():
     B = w.Theta.shape[1]
     eng = Engine(dev.index)
     eng.set_panel(w.Y, w.mats)
+    PREC = {"certified": _lib.PREC_CERTIFIED, "fp64": _lib.PREC_FP64}
+    eng.precision = PREC[args.precision]
     d_th = torch.from_numpy(np.ascontiguousarray(w.Theta.T)).to(dev)  # (B, P) C-order == P×B column-major
     d_tu = torch.from_numpy(w.T_use).to(dev) if w.T_use is not None else None
     d_out = torch.empty(B, dtype=torch.float64, device=dev)
@@ -271,45 +389,54 @@ def main():
             D.best_candidate_device(o, offset)
             c_done[i].record(stream)
 
-    for e in c_done:
-        e.record(stream)
-    for _ in range(args.warmup):
-        step()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    timing[0] = True
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    comp.wait_stream(stream)
-    for _ in range(args.steps):
-        step()
-    stream.wait_stream(comp)
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    wall = time.perf_counter() - t0
-    timing[0] = False
-    if world > 1:
-        t = torch.tensor([wall], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
-    # kernel time of one batch: HIP events around each launch in the timed region, on its stream
-    kernel_ms = float(np.mean([ks.elapsed_time(ke) for ks, ke in k_times]))
+    def timed(steps, warmup):
+        """warmup untimed steps, then `steps` timed ones between barriers; (wall s, mean kernel ms)."""
+        k_times.clear()
+        for e in c_done:
+            e.record(stream)
+        for _ in range(warmup):
+            step()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        timing[0] = True
+        t0 = time.perf_counter()
+        comp.wait_stream(stream)
+        for _ in range(steps):
+            step()
+        stream.wait_stream(comp)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        wall = time.perf_counter() - t0
+        timing[0] = False
+        if world > 1:
+            t = torch.tensor([wall], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            wall = float(t.item())
+        # kernel time of one batch: HIP events around each launch in the timed region, on its stream
+        return wall, float(np.mean([ks.elapsed_time(ke) for ks, ke in k_times]))
 
+    wall, kernel_ms = timed(args.steps, args.warmup)
     ms_per_step = 1e3 * wall / args.steps
     value = w.global_batch / (wall / args.steps)
-    f_rank = float(np.sum(alg_flops(kind, N, M, w.T_use if w.T_use is not None else T)) if w.T_use is not None
-                   else alg_flops(kind, N, M, T) * B)
-    achieved = f_rank / (kernel_ms * 1e-3) / 1e12  # TFLOP/s of this GPU's launches
-    traffic, traffic_src = pmc_traffic(DOMINANT[kind])
-    exe = pmc_executed_flops(DOMINANT[kind])
-    steps = float(np.sum(w.T_use - 1)) if w.T_use is not None else float(B * (T - 1))
-    exe_tf = exe * steps / (kernel_ms * 1e-3) / 1e12 if exe else None
+    roof = roofline(kind, args.precision, N, M, T, w.T_use, B, P, kernel_ms)
     out_host = d_out.cpu().numpy()
     n_neginf, n_nan = int(np.isneginf(out_host).sum()), int(np.isnan(out_host).sum())
+
+    # TVλ: the FP64 mode of the same workload beside the certified default (not the metric's value)
+    fp64_mode = None
+    if kind == KIND_TVL and args.precision == "certified":
+        eng.precision = _lib.PREC_FP64
+        wall64, kms64 = timed(args.steps, max(1, args.warmup // 2))
+        f64_host = d_out.cpu().numpy()
+        eng.precision = PREC[args.precision]
+        fin = np.isfinite(out_host)
+        d64 = np.abs(f64_host[fin] - out_host[fin]) / np.abs(out_host[fin])
+        fp64_mode = {"evals_per_s": w.global_batch / (wall64 / args.steps), "ms_per_step": 1e3 * wall64 / args.steps,
+                     "roofline": roofline(kind, "fp64", N, M, T, w.T_use, B, P, kms64),
+                     "vs_certified": {"frac_within_1e-9": float(np.mean(d64 <= 1e-9)), "max_rel": float(d64.max()),
+                                      "pattern_match": bool(np.array_equal(np.isfinite(f64_host), fin))}}
 
     # host-pointer boundary (yfm_loglik_batch: θ in over PCIe, logliks back, synchronous) —
     # reported beside the metric, never as `value` (inputs are not HBM-resident there)
@@ -347,21 +474,17 @@ def main():
             "config": {"workload": w.label, "kind": {KIND_DNS: "DNS (1C)", KIND_TVL: "TVλ (EKF)",
                                                       KIND_GNS: "GNS5 (extension)"}[kind],
                        "T": T, "N": N, "batch_per_gpu": B, "global_batch": w.global_batch,
+                       "precision": ("certified (double-double)" if args.precision == "certified" else "fp64")
+                       if kind == KIND_TVL else "fp64",
                        "parallelism": f"dp{world} (θ sharded, RCCL "
                                       f"{'all-gather of logliks + ' if w.gather else ''}argmax)", **w.extra},
-            "roofline": {"bound": "fp64-valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
-                         "algorithmic_bytes": B * (P + 1) * 8 + T * (N + 4) * 8,
-                         "kernel_ms": kernel_ms, "flops_per_eval": f_rank / max(B, 1),
-                         "executed_tflops": exe_tf, "executed_frac": exe_tf / FP64_PEAK_TFLOPS if exe_tf else None,
-                         "note": "achieved = SURVEY §8d algorithmic flops of this GPU's batch ÷ HIP-event time of its "
-                                 "launches on the library stream; the §8d count is for the capacitance form, this "
-                                 "build's collapsed form executes about half of it (executed_* = PMC-counted FP64 "
-                                 "flops of the same launch from profiles/, which is why frac can exceed 1)"},
+            "roofline": roof,
             "cpu_baseline": cpu,
             "host_pointer_rate": host_rate,
             "outputs": {"neg_inf": n_neginf, "nan": n_nan},
         }
+        if fp64_mode:
+            line["fp64_mode"] = fp64_mode
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
