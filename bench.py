@@ -135,12 +135,11 @@ def make_workload(config: int, world: int, rank: int, T: int, batch: int | None)
     if config == 5:
         total = batch or 1 << 20
         lo, hi = D.shard_range(total, world, rank)
-        # θ_b for b in [lo, hi) of the global search (generated per shard from the global seed stream)
-        Th_all = S.theta_batch(KIND_GNS, hi, seed=S.BATCH_SEED, bad_frac=0.0, scale=0.1)
+        # θ_b for b in [lo, hi) of the global search: candidate b depends only on (seed, b)
         mats = S.maturities_30()
         return Workload(5, KIND_GNS, f"config5: 5-factor GNS global search, {total:,} candidates split over "
                         f"{world} GPU(s), RCCL argmax", mats, S.simulate_panel(KIND_GNS, T),
-                        np.asfortranarray(Th_all[:, lo:hi]), None, total, "strong", False, {"offset": lo})
+                        S.theta_range(KIND_GNS, lo, hi, scale=0.1), None, total, "strong", False, {"offset": lo})
     raise ValueError(config)
 
 
@@ -328,17 +327,26 @@ def main():
                     help="TVλ arithmetic (include/yfm.h yfm_set_precision; the library default is certified)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="nccl = RCCL over xGMI (one GPU per rank); gloo = host collectives, ranks may share a GPU "
+                         "(multi-rank rehearsal on a one-GPU box)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 and args.dist_backend == "nccl":
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        gpu = local
+    elif world > 1:  # gloo rehearsal: ranks may share GPUs (collectives through host memory)
+        gpu = local % torch.cuda.device_count()
+        torch.cuda.set_device(gpu)
+        dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
+        gpu = 0
+    dev = torch.device("cuda", gpu)
 
     w = make_workload(args.config, world, rank, args.T, args.batch)
     kind = w.kind
@@ -366,6 +374,7 @@ def main():
     k_times = []  # (start, end) HIP events around each timed launch, on the launch stream
     timing = [False]
     it = [0]
+    best = [None]  # [loglik, global index] of the last step's argmax reduction (N > 1)
 
     def step():
         i = it[0] % len(outs)
@@ -386,7 +395,7 @@ def main():
             stream.wait_event(k_done[i])
             if w.gather:
                 D.gather_logliks(o, counts)
-            D.best_candidate_device(o, offset)
+            best[0] = D.best_candidate_device(o, offset)
             c_done[i].record(stream)
 
     def timed(steps, warmup):
@@ -418,6 +427,7 @@ def main():
         return wall, float(np.mean([ks.elapsed_time(ke) for ks, ke in k_times]))
 
     wall, kernel_ms = timed(args.steps, args.warmup)
+    best_main = best[0]
     ms_per_step = 1e3 * wall / args.steps
     value = w.global_batch / (wall / args.steps)
     roof = roofline(kind, args.precision, N, M, T, w.T_use, B, P, kernel_ms)
@@ -485,6 +495,8 @@ def main():
         }
         if fp64_mode:
             line["fp64_mode"] = fp64_mode
+        if best_main is not None:
+            line["best_candidate"] = {"loglik": float(best_main[0].item()), "index": int(best_main[1].item())}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -184,3 +184,21 @@ def test_sharded_estimate_equals_single_process():
     mp.spawn(_estimate_worker, args=(2, _free_port(), Theta0, T_use, Y, mats, ret), nprocs=2, join=True)
     np.testing.assert_array_equal(ret["theta_c"], ret["single_theta_c"])
     np.testing.assert_array_equal(ret["ll"], ret["single_ll"])
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_config5_shards_are_the_single_gpu_candidates(world):
+    """Strong scaling evaluates the same job at every world size: the rank shards of bench config 5,
+    concatenated in rank order, are exactly the single-GPU candidate matrix (candidate b depends
+    only on (seed, b): yfm_amd.synthetic.theta_range)."""
+    import bench
+    one = bench.make_workload(5, 1, 0, 30, 5000).Theta
+    parts = [bench.make_workload(5, world, r, 30, 5000).Theta for r in range(world)]
+    np.testing.assert_array_equal(np.hstack(parts), one)
+
+
+def test_theta_range_blocks_are_consistent():
+    from yfm_amd import synthetic as S
+    full = S.theta_range(2, 0, 2 * S.RANGE_BLOCK + 10)
+    np.testing.assert_array_equal(S.theta_range(2, S.RANGE_BLOCK - 3, S.RANGE_BLOCK + 7),
+                                  full[:, S.RANGE_BLOCK - 3:S.RANGE_BLOCK + 7])

@@ -51,15 +51,22 @@ class GatherResult:
     best_value: float
 
 
+def _comm_device(group, device) -> torch.device:
+    """Where a collective's buffers live: the tensors' own device for nccl (RCCL over xGMI), the
+    host for gloo (CPU tests, and multi-rank rehearsals that share one GPU)."""
+    return torch.device("cpu") if dist.get_backend(group) == "gloo" else device
+
+
 def gather_logliks(local: torch.Tensor, counts: list[int], group=None) -> torch.Tensor:
     """All-gather per-rank loglik vectors of (possibly unequal) `counts` into global rank order."""
     world = dist.get_world_size(group)
     m = max(counts)
-    buf = torch.full((m,), float("nan"), dtype=local.dtype, device=local.device)
-    buf[: local.numel()] = local
-    out = torch.empty(world * m, dtype=local.dtype, device=local.device)
+    cdev = _comm_device(group, local.device)
+    buf = torch.full((m,), float("nan"), dtype=local.dtype, device=cdev)
+    buf[: local.numel()] = local.to(cdev)
+    out = torch.empty(world * m, dtype=local.dtype, device=cdev)
     dist.all_gather_into_tensor(out, buf, group=group)
-    return torch.cat([out[r * m: r * m + counts[r]] for r in range(world)])
+    return torch.cat([out[r * m: r * m + counts[r]] for r in range(world)]).to(local.device)
 
 
 def best_candidate(local: torch.Tensor, global_offset: int, group=None) -> tuple[int, float]:
@@ -71,8 +78,9 @@ def best_candidate(local: torch.Tensor, global_offset: int, group=None) -> tuple
     else:
         pair = torch.tensor([-float("inf"), float("inf")], dtype=torch.float64, device=local.device)
     world = dist.get_world_size(group)
-    allp = torch.empty(2 * world, dtype=torch.float64, device=local.device)
-    dist.all_gather_into_tensor(allp, pair, group=group)
+    cdev = _comm_device(group, local.device)
+    allp = torch.empty(2 * world, dtype=torch.float64, device=cdev)
+    dist.all_gather_into_tensor(allp, pair.to(cdev), group=group)
     allp = allp.view(world, 2).cpu().numpy()
     best = max(range(world), key=lambda r: (allp[r, 0], -allp[r, 1]))
     return int(allp[best, 1]), float(allp[best, 0])
@@ -82,15 +90,19 @@ def best_candidate_device(local: torch.Tensor, global_offset: int, group=None) -
     """Same reduction as `best_candidate` without a host round trip (for timed loops): returns a
     device tensor [best loglik, global index].  Every rank contributes (max, its global index);
     one all-gather of 16 B per rank; the first maximal pair in rank order wins (lowest index)."""
-    v = torch.nan_to_num(local, nan=-float("inf"))
-    i = torch.argmax(v)
-    pair = torch.stack([v[i], (i + global_offset).to(torch.float64)])
+    if local.numel():
+        v = torch.nan_to_num(local, nan=-float("inf"))
+        i = torch.argmax(v)
+        pair = torch.stack([v[i], (i + global_offset).to(torch.float64)])
+    else:  # an empty shard (B < world size) still takes part in the all-gather
+        pair = torch.tensor([-float("inf"), float("inf")], dtype=torch.float64, device=local.device)
     world = dist.get_world_size(group)
-    allp = torch.empty(2 * world, dtype=torch.float64, device=local.device)
-    dist.all_gather_into_tensor(allp, pair, group=group)
+    cdev = _comm_device(group, local.device)
+    allp = torch.empty(2 * world, dtype=torch.float64, device=cdev)
+    dist.all_gather_into_tensor(allp, pair.to(cdev), group=group)
     allp = allp.view(world, 2)
     r = torch.argmax(allp[:, 0])
-    return allp[r]
+    return allp[r].to(local.device)
 
 
 def sharded_loglik(Theta: np.ndarray, evaluate: Callable[[np.ndarray], torch.Tensor], group=None,
@@ -144,7 +156,7 @@ def sharded_estimate(Theta0: np.ndarray, T_use, estimate: Callable, group=None, 
     buf = torch.full((P + 2, m), float("nan"), dtype=torch.float64)
     buf[:, :local.shape[1]] = torch.from_numpy(local)
     if device is not None:
-        buf = buf.to(device)
+        buf = buf.to(_comm_device(group, device))
     out = torch.empty((world * (P + 2), m), dtype=torch.float64, device=buf.device)
     dist.all_gather_into_tensor(out, buf.contiguous(), group=group)
     out = out.view(world, P + 2, m).cpu().numpy()

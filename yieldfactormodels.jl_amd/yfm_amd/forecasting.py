@@ -175,8 +175,8 @@ def run_rolling_forecasts(model, data, thread_id: str, in_sample_end: int, in_sa
                           forecast_horizon: int, init_params, window_type: str = "both", max_group_iters: int = 10,
                           group_tol: float = 1e-8, reestimate: bool = True, params=None, iterations: int = 500,
                           write_csv: bool = True, group=None) -> dict:
-    """forecasting.jl:16-51.  Returns {window_type: result dict}; writes the reference's CSVs when
-    write_csv.  With window_type "both" the per-task estimation (identical for both window types,
+    """forecasting.jl:16-51.  Returns {window_type: result dict} (on rank 0 of `group`; {} on the
+    other ranks); writes the reference's CSVs when write_csv.  With window_type "both" the per-task estimation (identical for both window types,
     both use the expanding sample) runs once and is shared.  `group`: a torch.distributed process
     group (one process per GPU) over which the per-task estimation chains are split (the
     reference's multi-process task claiming, forecasting.jl:54-79, done as one sharded batch)."""
@@ -191,7 +191,13 @@ def run_rolling_forecasts(model, data, thread_id: str, in_sample_end: int, in_sa
     est = None
     if reestimate:
         est = _estimate_tasks(model, data, tasks, init_params, max_group_iters, group_tol, iterations, group)
+    # with a group, every rank holds every task's estimate after the all-gather; the predict pass
+    # and the CSV files (one set of paths per model / thread_id) belong to rank 0 alone, so ranks
+    # never truncate-and-write the same files concurrently
+    lead = group is None or _rank(group) == 0
     out = {}
+    if not lead:
+        return out
     for wt in kinds:
         res = forecast_windows(model, data, in_sample_end, in_sample_start, forecast_horizon, wt, init_params,
                                max_group_iters, group_tol, reestimate, params, iterations, estimates=est)
@@ -199,3 +205,8 @@ def run_rolling_forecasts(model, data, thread_id: str, in_sample_end: int, in_sa
             res["files"] = write_window_csvs(model, thread_id, res)
         out[wt] = res
     return out
+
+
+def _rank(group) -> int:
+    import torch.distributed as dist
+    return dist.get_rank(group)

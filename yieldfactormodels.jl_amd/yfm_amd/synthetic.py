@@ -151,3 +151,25 @@ def theta_batch(kind: int = KIND_DNS, B: int = 65536, scale: float = 0.1, seed: 
         Theta[lay.phi_offset + 1, idx] = a  # Φ[1,2] (row-major)
         Theta[lay.phi_offset + lay.M, idx] = np.where(a == 0.8, 0.8, -3.0)  # Φ[2,1]
     return Theta
+
+
+RANGE_BLOCK = 65536
+
+
+def theta_range(kind: int, lo: int, hi: int, scale: float = 0.1, seed: int = BATCH_SEED) -> np.ndarray:
+    """Columns [lo, hi) of a global candidate stream (P×(hi−lo), F-order) in which candidate b
+    depends only on (seed, b): blocks of RANGE_BLOCK candidates each draw θ₀ + scale·N(0, I) from
+    their own generator PCG64([seed, block]).  Any shard of a job (bench config 5 split over G
+    GPUs) therefore evaluates exactly the candidates a single GPU would."""
+    P = n_params(kind)
+    th0 = theta0(kind)
+    out = np.empty((P, max(hi - lo, 0)), order="F")
+    b = lo
+    while b < hi:
+        k = b // RANGE_BLOCK
+        rng = np.random.Generator(np.random.PCG64([seed, k]))
+        blk = th0[:, None] + scale * rng.standard_normal((RANGE_BLOCK, P)).T
+        a, e = b - k * RANGE_BLOCK, min(hi - k * RANGE_BLOCK, RANGE_BLOCK)
+        out[:, b - lo:b - lo + (e - a)] = blk[:, a:e]
+        b += e - a
+    return out
