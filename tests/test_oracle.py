@@ -252,3 +252,20 @@ def test_quad_truth_tvl_n360_summation_order_invariant():
     b = loglik_truth(KIND_TVL, Y[::-1], mats[::-1], Th)
     assert np.all(np.isfinite(a))
     assert rel_err(a, b) <= 1e-15
+
+
+def test_edge_fixtures_reproduce():
+    """tests/golden/edge/edge_cases.npz holds the NumPy/LAPACK oracle's and the binary128 truth's
+    values (generator: tests/golden/edge/make_edge.py)."""
+    from oracle.truth import loglik_truth
+    with np.load(ROOT / "tests" / "golden" / "edge" / "edge_cases.npz", allow_pickle=False) as z:
+        fx = {k: z[k] for k in z.files}
+    for name in fx["names"]:
+        c = {k.split("/", 1)[1]: v for k, v in fx.items() if k.startswith(f"{name}/")}
+        kind, space, tu = int(c["kind"]), int(c["space"]), c.get("T_use")
+        tru = loglik_truth(kind, c["Y"], c["maturities"], c["Theta"], space=space, T_use=tu)
+        np.testing.assert_array_equal(tru, c["loglik_truth"])
+        for b in range(min(2, c["Theta"].shape[1])):
+            Yb = c["Y"] if tu is None else c["Y"][:, :tu[b]]
+            ll = O.loglik(kind, c["maturities"], state_dim(kind), Yb, c["Theta"][:, b], space=space)
+            assert ll == c["loglik_oracle"][b] or (np.isnan(ll) and np.isnan(c["loglik_oracle"][b]))
