@@ -460,8 +460,19 @@ def main():
         for _ in range(reps):
             eng.loglik(kind, Th_host, space=0, T_use=tu_host)
         host_s = (time.perf_counter() - th0) / reps
+        # the same with θ and the logliks in page-locked memory (yfm_alloc_host)
+        th_pin = eng.host_array(Th_host.shape)
+        th_pin[...] = Th_host
+        out_pin = eng.host_array((B,))
+        eng.loglik(kind, th_pin, space=0, T_use=tu_host, out=out_pin)
+        th0 = time.perf_counter()
+        for _ in range(reps):
+            eng.loglik(kind, th_pin, space=0, T_use=tu_host, out=out_pin)
+        pin_s = (time.perf_counter() - th0) / reps
         host_rate = {"evals_per_s": B / host_s, "ms_per_call": 1e3 * host_s, "calls": reps,
-                     "note": "yfm_loglik_batch with host θ / host logliks (H2D + kernel + D2H, synchronous)"}
+                     "pinned_evals_per_s": B / pin_s, "pinned_ms_per_call": 1e3 * pin_s,
+                     "note": "yfm_loglik_batch with host θ / host logliks (H2D + kernel + D2H, synchronous); "
+                             "pinned_* with both in yfm_alloc_host memory"}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -29,6 +29,8 @@
 #ifndef YFM_H
 #define YFM_H
 
+#include <stddef.h>
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -86,6 +88,12 @@ void yfm_destroy(yfm_ctx* ctx);
  * The reference has no such switch: its Float64 path is YFM_PREC_FP64's arithmetic class. */
 int yfm_set_precision(yfm_ctx* ctx, int precision);
 int yfm_get_precision(yfm_ctx* ctx);
+
+/* Page-locked host memory for the host-pointer entry points: θ batches and output buffers
+ * allocated here are copied by DMA without a staging pass (the caller keeps the Julia/Python
+ * array view; free with yfm_free_host).  NULL on failure (yfm_last_error). */
+void* yfm_alloc_host(size_t bytes);
+int yfm_free_host(void* p);
 
 /* Upload the yield panel.  Y: N×T column-major (the `data` argument of get_loss,
  * filter.jl:182); maturities: N (KalmanBaseModel.maturities).  Copied; the
@@ -160,13 +168,16 @@ int yfm_loss_array(yfm_ctx* ctx, int model_kind, int param_space, const double* 
  * constrained all_params and untransforms them) on the window Y[:, 1:T_use[r]] (or all
  * T columns when T_use is NULL).  The R chains' objective evaluations are batched into
  * one device launch per round.  Outputs: theta_c_out P×R = transform_params(best_p)
- * (the reference's returned params), p_out P×R unconstrained optimum (or NULL), ll_out R
+ * (the reference's returned params), p_out P×R unconstrained optimum (or NULL), init_c_out P×R
+ * (or NULL) = transform_params of the sanitised, ×0.95-rescaled start (the reference's returned
+ * init_p, optimization.jl:157-184, :298-302), ll_out R
  * (the reference's returned ll), status_out R (or NULL): 0 ok, 1 the reference would
  * throw (NaN outputs), 2 aborted after the first group iteration (parameters kept);
  * n_evals_out (or NULL): objective evaluations performed.  Synchronous. */
 int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const double* theta0, int P, int R,
                  const int* T_use, int iterations, double g_tol, int max_group_iters, double tol,
-                 double* theta_c_out, double* p_out, double* ll_out, int* status_out, long long* n_evals_out);
+                 double* theta_c_out, double* p_out, double* init_c_out, double* ll_out, int* status_out,
+                 long long* n_evals_out);
 
 /* Counters of the last completed batch on this ctx: candidates where the
  * reference would have thrown (NaN outputs) and candidates returning -Inf.

@@ -123,51 +123,29 @@ def test_estimate_steps_model_api(engine, panel):
     model, _ = create_model("1C", mats, 30)
     th0 = S.theta0_constrained(KIND_DNS)
     init_p, ll, best_p, ir = estimate_steps_(model, Y, th0[:, None], ["1"] * 20, max_group_iters=1)
-    np.testing.assert_array_equal(init_p, th0)
+    np.testing.assert_allclose(init_p, th0, rtol=1e-14)  # transform(untransform(th0)): rounding only
     set_params_(model, best_p)
     assert abs(get_loss(model, Y) - ll) <= 1e-12 * abs(ll)
     set_params_(model, th0)
     assert ll > get_loss(model, Y)
 
 
-def test_rolling_forecasts_driver(engine, tmp_path):
-    """run_rolling_forecasts (forecasting.jl:16-51, :81-224) for "both" window types: the batched
-    per-task estimation equals each task's chain run alone, the forecast records equal the oracle's
-    predict on hcat(window, NaN × (h−1)) rounded to 3 digits, and the six export CSVs per window
-    type have the reference's names and layouts."""
-    from oracle import kalman_oracle as O
-    from yfm_amd import create_model
-    from yfm_amd import io as yio
-    from yfm_amd.forecasting import run_rolling_forecasts
-    mats = S.maturities_30()
-    Y = S.simulate_panel(KIND_DNS, 600)[:, :56].copy(order="F")
-    model, _ = create_model("1C", mats, 30, results_location=str(tmp_path) + "/")
-    th0 = S.theta0_constrained(KIND_DNS)
-    h = 3
-    out = run_rolling_forecasts(model, Y, "9", 50, 11, h, th0[:, None], window_type="both", max_group_iters=1,
-                                iterations=25)
-    ex, mv = out["expanding"], out["moving"]
-    tasks = np.arange(50, 57)
-    np.testing.assert_array_equal(ex["tasks"], tasks)
-    np.testing.assert_array_equal(ex["params"], mv["params"])  # both use the expanding sample (:165)
-    engine.set_panel(Y, mats)  # the moving-window forecasts left a window panel on the engine
-    one = engine.estimate(KIND_DNS, th0, space=1, T_use=[53], iterations=25, max_group_iters=1)
-    np.testing.assert_array_equal(one["theta_c"][:, 0], ex["params"][:, 3])
-    assert one["ll"][0] == ex["loss"][3]
-    for i, task in enumerate(tasks):
-        for wt, res, lo in (("expanding", ex, 0), ("moving", mv, task - 39 - 1)):
-            s = O.KalmanState.fresh(KIND_DNS, mats, 3)
-            O.set_params(s, res["params"][:, i])
-            r = O.predict(s, O.pad_nan(Y[:, lo:task], h))
-            for k in ("preds", "factors", "factor_loadings_1"):
-                ref = yio.julia_round(r[k][:, -h:], 3)
-                assert np.abs(res[k][:, :, i] - ref).max() <= 1.0001e-3, (wt, k, task)
-                assert (res[k][:, :, i] == ref).mean() > 0.9
-    for wt in ("expanding", "moving"):
-        f = yio.readdlm(tmp_path / f"1C__thread_id__9__{wt}_window_forecasts.csv")
-        assert f.shape == (len(tasks) * h, 2 + 30)
-        np.testing.assert_array_equal(f[:4, :2], [[50, 51], [50, 52], [50, 53], [51, 52]])
-        p = yio.readdlm(tmp_path / f"1C__thread_id__9__{wt}_window_fitted_params.csv")
-        assert p.shape == (len(tasks), 21)
-        st = yio.readdlm(tmp_path / f"1C__thread_id__9__{wt}_window_states.csv")
-        assert st.shape == (len(tasks) * h, 3)
+def test_estimate_init_is_the_rescaled_start(engine, panel):
+    """A start whose loglik is not finite (unconstrained Φ₁₁ = 800: from_R_to_11 overflows to
+    Inf/Inf = NaN) is multiplied by 0.95 in the unconstrained space until it is (three times here,
+    optimization.jl:173-184); the chain's init_p is that start transformed back (:298-302)."""
+    from yfm_amd.params import param_layout, transform_params
+    Y, mats = panel
+    lay = param_layout(KIND_DNS)
+    p = S.theta0(KIND_DNS).copy()
+    p[lay.phi_offset] = 800.0
+    engine.set_panel(Y, mats)
+    q = p.copy()
+    k = 0
+    while not np.isfinite(engine.loglik(KIND_DNS, q, space=0)[0]):
+        q = q * 0.95
+        k += 1
+    assert k == 3
+    r = engine.estimate(KIND_DNS, p[:, None], space=0, iterations=20, max_group_iters=1)
+    assert r["status"][0] == 0 and np.isfinite(r["ll"][0])
+    np.testing.assert_allclose(r["init_c"][:, 0], transform_params(KIND_DNS, q), rtol=1e-13)

@@ -250,3 +250,18 @@ def test_model_api_mirror(engine, headline):
     Th = S.theta_batch(KIND_DNS, 16, seed=2, bad_frac=0.0)
     cl = compute_loss_batch(model, Y, Th)
     assert abs(-cl[0] - O.loglik(KIND_DNS, mats, 3, Y, Th[:, 0])) <= REL * abs(cl[0])
+
+
+def test_pinned_host_buffers(engine, headline):
+    """yfm_alloc_host / yfm_free_host: θ and logliks in page-locked memory give the same bits."""
+    Y, mats = headline
+    engine.set_panel(Y, mats)
+    Th = S.theta_batch(KIND_DNS, 5000, seed=17)
+    ref = engine.loglik(KIND_DNS, Th)
+    th_pin = engine.host_array(Th.shape)
+    th_pin[...] = Th
+    out = engine.host_array((5000,))
+    got = engine.loglik(KIND_DNS, th_pin, out=out)
+    assert got is out
+    np.testing.assert_array_equal(out, ref)
+    del th_pin, out, got

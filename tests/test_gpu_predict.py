@@ -224,9 +224,9 @@ def test_trajectory_api_errors(engine, panel):
     assert lib.yfm_forecast(engine.ctx, 0, 1, D(th), 20, 2, _lib.iptr(bad), 2, D(out)) == -1
     st = np.zeros(2, dtype=np.int32)
     ll = np.zeros(2)
-    assert lib.yfm_estimate(engine.ctx, 0, 1, D(th), 20, 2, None, 10, 1e-6, 0, 1e-8, D(out), None, D(ll),
+    assert lib.yfm_estimate(engine.ctx, 0, 1, D(th), 20, 2, None, 10, 1e-6, 0, 1e-8, D(out), None, None, D(ll),
                             _lib.iptr(st), None) == -1  # max_group_iters < 1
-    assert lib.yfm_estimate(engine.ctx, 0, 5, D(th), 20, 2, None, 10, 1e-6, 1, 1e-8, D(out), None, D(ll),
+    assert lib.yfm_estimate(engine.ctx, 0, 5, D(th), 20, 2, None, 10, 1e-6, 1, 1e-8, D(out), None, None, D(ll),
                             _lib.iptr(st), None) == -1  # param_space
     assert lib.yfm_gamma_dim(0) == 1 and lib.yfm_gamma_dim(1) == 1 and lib.yfm_gamma_dim(2) == 2
     assert lib.yfm_gamma_dim(7) == -1

@@ -377,6 +377,22 @@ void yfm_destroy(yfm_ctx* ctx) {
   delete ctx;
 }
 
+void* yfm_alloc_host(size_t bytes) {
+  void* p = nullptr;
+  hipError_t e = hipHostMalloc(&p, bytes > 0 ? bytes : 1, hipHostMallocPortable);
+  if (e != hipSuccess) {
+    set_error(YFM_EHIP, "hipHostMalloc(%zu): %s", bytes, hipGetErrorString(e));
+    return nullptr;
+  }
+  return p;
+}
+
+int yfm_free_host(void* p) {
+  if (!p) return YFM_OK;
+  YFM_HIP_CHECK(hipHostFree(p));
+  return YFM_OK;
+}
+
 int yfm_set_precision(yfm_ctx* ctx, int precision) {
   if (int r = check_ctx(ctx)) return r;
   if (precision != YFM_PREC_CERTIFIED && precision != YFM_PREC_FP64)

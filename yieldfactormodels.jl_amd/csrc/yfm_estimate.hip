@@ -92,6 +92,7 @@ double to_unconstrained(int code, double x) {
 enum Phase { VALIDATE, NM_INIT, NM_ITER, NM_SHRINK, NM_FINAL, DONE };
 
 struct Chain {
+  std::vector<double> start;  // unconstrained start after sanitising and ×0.95 rescaling
   int n = 0;                // parameters (simplex dimension)
   Phase phase = VALIDATE;
   int window = 0;           // T_use of this chain
@@ -245,6 +246,7 @@ void consume(Chain& c, const double* f, int max_group_iters, double tol, double 
         return;
       }
       c.outer = 1;
+      c.start = c.p;  // the sanitised, rescaled start: estimate_steps!'s init_p (optimization.jl:281, :298-302)
       c.phase = NM_INIT;
       return;
     }
@@ -358,8 +360,8 @@ void consume(Chain& c, const double* f, int max_group_iters, double tol, double 
 
 extern "C" int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const double* theta0, int P, int R,
                             const int* T_use, int iterations, double g_tol, int max_group_iters, double tol,
-                            double* theta_c_out, double* p_out, double* ll_out, int* status_out,
-                            long long* n_evals_out) {
+                            double* theta_c_out, double* p_out, double* init_c_out, double* ll_out,
+                            int* status_out, long long* n_evals_out) {
   if (!ctx) return yfm::api_error(YFM_EINVAL, "null context");
   if (yfm_param_count(model_kind) < 0) return yfm::api_error(YFM_EINVAL, "unknown model_kind");
   if (P != yfm_param_count(model_kind)) return yfm::api_error(YFM_EINVAL, "P does not match model_kind");
@@ -415,6 +417,8 @@ extern "C" int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const
     for (int i = 0; i < P; ++i) {
       theta_c_out[(size_t)r * P + i] = ok ? to_constrained(codes[i], c.p[i]) : NAN;
       if (p_out) p_out[(size_t)r * P + i] = c.p[i];
+      if (init_c_out)
+        init_c_out[(size_t)r * P + i] = (ok && !c.start.empty()) ? to_constrained(codes[i], c.start[i]) : NAN;
     }
     ll_out[r] = ok ? c.prev_ll : NAN;
     if (status_out) status_out[r] = c.status;

@@ -18,7 +18,7 @@
 // — and the group reduces them with DPP / permlane butterflies (no LDS).  Every lane
 // of the group then runs the same 4×4 capacitance update redundantly, so the state
 // stays replicated in VGPRs and no broadcast is needed.  L is chosen per launch so
-// that B·L lanes fill the chip (B = 16,384 → L = 4; B = 1,024 → L = 64; B = 1 → L = 64).
+// that B·L lanes fill the chip at two waves per SIMD (B = 16,384 → L = 8; B = 1,024 → L = 64).
 //
 // Capacitance form (nothing N×N is formed): B̃ = σ²I + P G, W = B̃⁻¹P,
 //   K v = W u,  P_{t|t} = σ² W,  v'F⁻¹v = (v'v − u'Wu)/σ²,
@@ -381,10 +381,10 @@ size_t tvl_scratch_bytes(int B) { return sizeof(double) * (size_t)kRecLen * (siz
 int tvl_max_n() { return (kTvlPre * kTvlBlock) - 1; }
 
 int tvl_lanes_for(int B, int N) {
-  // enough lanes for two waves per SIMD (256 CUs × 4 SIMDs × 2 × 64 lanes — the kernel is
-  // built for two; measured on MI355X at N = 360: B = 16,384 → L = 8 (5.77 ms vs 6.06 ms at
-  // L = 4 and 7.65 ms at L = 16, steady clock, profiles/r1/final/tvl_lanes), B = 65,536 → L = 2), capped at a wave and at the maturity count rounded up to a
-  // power of two
+  // enough lanes for two waves per SIMD (256 CUs × 4 SIMDs × 2 × 64 lanes — the kernel is built
+  // for two), capped at a wave and at the maturity count rounded up to a power of two.  Measured
+  // on MI355X at N = 360, steady clock (profiles/r1/final/tvl_lanes): B = 16,384 → L = 8 takes
+  // 5.77 ms vs 6.06 ms at L = 4 and 7.65 ms at L = 16; B = 65,536 → L = 2.
   long long want = (2048LL * 64 + B - 1) / (B > 0 ? B : 1);
   int L = 1;
   while (L < want && L < 64) L <<= 1;

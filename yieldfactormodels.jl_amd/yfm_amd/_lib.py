@@ -39,7 +39,9 @@ SIGNATURES = {
     "yfm_forecast": (ctypes.c_int, [_V, ctypes.c_int, ctypes.c_int, _D, ctypes.c_int, ctypes.c_int, _I, ctypes.c_int,
                                     _D]),
     "yfm_estimate": (ctypes.c_int, [_V, ctypes.c_int, ctypes.c_int, _D, ctypes.c_int, ctypes.c_int, _I, ctypes.c_int,
-                                    ctypes.c_double, ctypes.c_int, ctypes.c_double, _D, _D, _D, _I, _LL]),
+                                    ctypes.c_double, ctypes.c_int, ctypes.c_double, _D, _D, _D, _D, _I, _LL]),
+    "yfm_alloc_host": (_V, [ctypes.c_size_t]),
+    "yfm_free_host": (ctypes.c_int, [_V]),
     "yfm_set_precision": (ctypes.c_int, [_V, ctypes.c_int]),
     "yfm_get_precision": (ctypes.c_int, [_V]),
     "yfm_loss_array": (ctypes.c_int, [_V, ctypes.c_int, ctypes.c_int, _D, ctypes.c_int, ctypes.c_int, _I, ctypes.c_int,

@@ -48,6 +48,21 @@ class Engine:
     def precision(self, mode: int) -> None:
         _lib.check(self.lib.yfm_set_precision(self.ctx, int(mode)))
 
+    # ---- page-locked host buffers (yfm_alloc_host) ----------------------------------
+    def host_array(self, shape, dtype=np.float64) -> np.ndarray:
+        """A Fortran-ordered array in page-locked host memory: θ batches and loglik outputs built in
+        it reach the device by DMA without a staging copy.  Freed when the array is collected."""
+        dtype = np.dtype(dtype)
+        n = int(np.prod(shape)) * dtype.itemsize
+        ptr = self.lib.yfm_alloc_host(n)
+        if not ptr:
+            raise _lib.YFMError(-2, self.lib.yfm_last_error().decode())
+        buf = (ctypes.c_char * n).from_address(ptr)
+        arr = np.frombuffer(buf, dtype=dtype).reshape(shape, order="F")
+        import weakref
+        weakref.finalize(buf, self.lib.yfm_free_host, ctypes.c_void_p(ptr))
+        return arr
+
     # ---- panel -------------------------------------------------------------------
     def set_panel(self, data, maturities, force: bool = False):
         """data: N×T (maturities × months) like the reference's ``data`` matrix."""
@@ -68,8 +83,9 @@ class Engine:
         return 0 if self._panel is None else self._panel.shape[1]
 
     # ---- batched evaluation ----------------------------------------------------------
-    def loglik(self, kind: int, theta, space: int = 0, T_use=None) -> np.ndarray:
-        """Θ: P×B (or a length-P vector).  Returns B logliks (+loglik, get_loss sign)."""
+    def loglik(self, kind: int, theta, space: int = 0, T_use=None, out=None) -> np.ndarray:
+        """Θ: P×B (or a length-P vector).  Returns B logliks (+loglik, get_loss sign), written into
+        `out` when given (e.g. a page-locked `host_array`)."""
         Th = np.asarray(theta, dtype=np.float64)
         if Th.ndim == 1:
             Th = Th[:, None]
@@ -77,7 +93,10 @@ class Engine:
         P, B = Th.shape
         if P != n_params(kind):
             raise ValueError(f"theta has {P} rows, model kind {kind} needs {n_params(kind)}")
-        out = np.empty(B, dtype=np.float64)
+        if out is None:
+            out = np.empty(B, dtype=np.float64)
+        elif out.shape != (B,) or out.dtype != np.float64 or not out.flags.c_contiguous:
+            raise ValueError("out must be a contiguous float64 vector of length B")
         tu = None if T_use is None else np.ascontiguousarray(np.broadcast_to(T_use, (B,)), dtype=np.int32)
         _lib.check(self.lib.yfm_loglik_batch(self.ctx, kind, space, _lib.dptr(Th), P, B, _lib.iptr(tu),
                                              _lib.dptr(out)))
@@ -156,18 +175,20 @@ class Engine:
     def estimate(self, kind: int, theta0, space: int = 1, T_use=None, iterations: int = 500, g_tol: float = 1e-6,
                  max_group_iters: int = 10, tol: float = 1e-8) -> dict:
         """Batched estimate_steps! (optimization.jl:137-312): one Nelder–Mead chain per column of Θ₀ (P×R),
-        on window T_use[r].  Returns theta_c (P×R), p (P×R unconstrained), ll (R), status (R), n_evals."""
+        on window T_use[r].  Returns theta_c (P×R), p (P×R unconstrained), init_c (P×R: the reference's
+        init_p — the sanitised, rescaled start, constrained), ll (R), status (R), n_evals."""
         Th = self._batch(theta0, kind)
         P, R = Th.shape
         th_c = np.empty((P, R), order="F")
         p = np.empty((P, R), order="F")
+        init_c = np.empty((P, R), order="F")
         ll = np.empty(R)
         st = np.empty(R, dtype=np.int32)
         ne = ctypes.c_longlong(0)
         _lib.check(self.lib.yfm_estimate(self.ctx, kind, space, _lib.dptr(Th), P, R, _lib.iptr(self._tuse(T_use, R)),
                                          iterations, g_tol, max_group_iters, tol, _lib.dptr(th_c), _lib.dptr(p),
-                                         _lib.dptr(ll), _lib.iptr(st), ctypes.byref(ne)))
-        return dict(theta_c=th_c, p=p, ll=ll, status=st, n_evals=ne.value)
+                                         _lib.dptr(init_c), _lib.dptr(ll), _lib.iptr(st), ctypes.byref(ne)))
+        return dict(theta_c=th_c, p=p, init_c=init_c, ll=ll, status=st, n_evals=ne.value)
 
     def last_flags(self):
         a, b = ctypes.c_longlong(0), ctypes.c_longlong(0)

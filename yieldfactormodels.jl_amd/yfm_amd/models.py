@@ -241,7 +241,9 @@ class EstimationError(RuntimeError):
 def estimate_steps_(model: AbstractKalmanModel, data, all_params, param_groups=None, max_group_iters: int = 10,
                     tol: float = 1e-8, printing: bool = False):
     """estimate_steps! (optimization.jl:137-312) for a Kalman model: all_params (P×n, constrained; Kalman
-    models use column 1 only, :153) → (init_p, ll, best_p, ir) with best_p constrained, like the reference.
+    models use column 1 only, :153) → (init_p, ll, best_p, ir), init_p and best_p constrained like the
+    reference: init_p = transform_params of the untransformed, sanitised and ×0.95-rescaled start
+    (:157-184, :298-302).
     Parameter groups other than all-"1" are not supported (the Kalman default, kalmanbasemodel.jl:150-159)."""
     A = np.asarray(all_params, dtype=np.float64)
     start = A[:, 0] if A.ndim == 2 else A
@@ -252,7 +254,7 @@ def estimate_steps_(model: AbstractKalmanModel, data, all_params, param_groups=N
         raise EstimationError("compute_loss threw on the first group iteration (singular initialize_filter)")
     if printing:
         print(f"✓ Best overall LL = {r['ll'][0]} from start 1")
-    return start.copy(), float(r["ll"][0]), r["theta_c"][:, 0].copy(), 0
+    return r["init_c"][:, 0].copy(), float(r["ll"][0]), r["theta_c"][:, 0].copy(), 0
 
 
 def estimate_batch(model: AbstractKalmanModel, data, Theta0, T_use=None, space: int = 1, iterations: int = 500,
