@@ -228,7 +228,7 @@ int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int 
     yfm::TvlGaps g;
     if (ctx->precision == YFM_PREC_CERTIFIED) {
       lanes = yfm::tvl_dd_lanes_for(B, ctx->N, std::getenv("YFM_TVL_LANES") ? lanes : 0);
-      YFM_HIP_CHECK(ctx->scratch_dd.ensure(yfm::tvl_dd_scratch_bytes(B)));
+      YFM_HIP_CHECK(ctx->scratch_dd.ensure(yfm::tvl_dd_scratch_bytes(B, a.T)));
       double* rdd = static_cast<double*>(ctx->scratch_dd.p);
       if (int r = tvl_gaps(ctx, lanes, g)) return r;
       e = yfm::launch_tvl_dd_init(a, rdd);

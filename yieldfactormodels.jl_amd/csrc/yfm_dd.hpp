@@ -69,6 +69,13 @@ __device__ __forceinline__ dd dd_mul(dd x, dd y) {
   p.lo = __builtin_fma(x.hi, y.lo, __builtin_fma(x.lo, y.hi, p.lo));
   return fast_two_sum(p.hi, p.lo);
 }
+// x·y left unnormalised (|lo| ≤ ~3u|hi|): for products that only feed sums and products,
+// whose error-free steps do not need a normalised operand
+__device__ __forceinline__ dd dd_mul_nn(dd x, dd y) {
+  dd p = two_prod(x.hi, y.hi);
+  p.lo = __builtin_fma(x.hi, y.lo, __builtin_fma(x.lo, y.hi, p.lo));
+  return p;
+}
 // x·d
 __device__ __forceinline__ dd dd_mul_d(dd x, double d) {
   dd p = two_prod(x.hi, d);
@@ -100,6 +107,12 @@ struct dd_acc {
   __device__ __forceinline__ void add_prod(dd a, dd b) {
     dd p = two_prod(a.hi, b.hi);
     p.lo = __builtin_fma(a.hi, b.lo, __builtin_fma(a.lo, b.hi, p.lo));
+    add(p);
+  }
+  // += a·d (d a double)
+  __device__ __forceinline__ void add_prod_d(dd a, double d) {
+    dd p = two_prod(a.hi, d);
+    p.lo = __builtin_fma(a.lo, d, p.lo);
     add(p);
   }
   __device__ __forceinline__ dd value() const { return two_sum(hi, lo); }  // |lo| may exceed |hi| after cancellation

@@ -50,9 +50,10 @@ hipError_t launch_tvl(const LaunchArgs& a, const TvlGaps& g, int lanes);
 constexpr int kRecSigma = 0, kRecDelta = 1, kRecPhi = 5, kRecQ = 21, kRecBeta = 31, kRecP = 35, kRecOk = 45;
 constexpr int kRecLen = 48;  // padded to 16-byte multiples
 // the same filter in double-double arithmetic (yfm_tvl_dd.hip), YFM_PREC_CERTIFIED: the init
-// kernel writes the per-candidate dd records into `rec_dd` (tvl_dd_scratch_bytes(B));
+// kernel writes the per-candidate dd records and the panel's dd column sums into `rec_dd`
+// (tvl_dd_scratch_bytes(B, T));
 // tvl_dd_lanes_for picks the lanes per filter (`want` > 0: a requested width, clamped)
-size_t tvl_dd_scratch_bytes(int B);
+size_t tvl_dd_scratch_bytes(int B, int T);
 int tvl_dd_lanes_for(int B, int N, int want);
 hipError_t launch_tvl_dd_init(const LaunchArgs& a, double* rec_dd);
 hipError_t launch_tvl_dd(const LaunchArgs& a, const double* rec_dd, const TvlGaps& g, int lanes);

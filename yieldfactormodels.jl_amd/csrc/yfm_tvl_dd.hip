@@ -313,9 +313,30 @@ __global__ __launch_bounds__(64) void tvl_dd_init_kernel(const double* __restric
   r[kDOk + 1] = 0.0;
 }
 
+// Σ_i y_it and Σ_i y_it² per panel column in dd (summed in maturity order; NaN columns give
+// NaN and are never read): colsum[4t .. 4t+3] = (Σy.hi, Σy.lo, Σy².hi, Σy².lo)
+__global__ __launch_bounds__(64) void tvl_dd_colsum_kernel(const double* __restrict__ Y, int N, int T,
+                                                           double* __restrict__ colsum) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= T) return;
+  const double* y = Y + (size_t)t * N;
+  dd_acc s1, s2;
+  for (int i = 0; i < N; ++i) {
+    const double v = y[i];
+    s1.add(dd_make(v));
+    s2.add(two_prod(v, v));
+  }
+  const dd a = s1.value(), b = s2.value();
+  colsum[4 * (size_t)t] = a.hi;
+  colsum[4 * (size_t)t + 1] = a.lo;
+  colsum[4 * (size_t)t + 2] = b.hi;
+  colsum[4 * (size_t)t + 3] = b.lo;
+}
+
 template <int L, bool RECORD>
 __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
-    const double* __restrict__ rec, int B, const double* __restrict__ Y, const double* __restrict__ prep, int ldp,
+    const double* __restrict__ rec, int B, const double* __restrict__ Y, const double* __restrict__ colsum,
+    const double* __restrict__ prep, int ldp,
     int np, int T, int N, int TC, const double* __restrict__ mats, int K, const double* __restrict__ gap_d,
     const int* __restrict__ gap_idx, const int* __restrict__ T_use, double* __restrict__ out, unsigned int* __restrict__ flags, double* __restrict__ rec_beta,
     double* __restrict__ rec_P, int horizon, int rec_len) {
@@ -324,7 +345,8 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
   double* s_m = smem;                                  // m_i
   dd* s_rm = reinterpret_cast<dd*>(smem + N);          // 1/m_i (dd)
   double* s_nan = smem + 3 * N;                        // TC NaN flags of the staged chunk
-  double* s_y = s_nan + TC;                            // TC columns of N yields
+  dd* s_sum = reinterpret_cast<dd*>(s_nan + TC);       // per staged column: Σy, Σy² (dd)
+  double* s_y = s_nan + 5 * TC;                        // TC columns of N yields
   double* s_par = s_y + TC * N;                        // per group: σ², δ, Φ, Q (kDPar doubles)
   dd* s_w = reinterpret_cast<dd*>(s_par + GPB * kDPar);  // per group: e^{-λ d_k}, k < K
   int* s_gi = reinterpret_cast<int*>(s_w + GPB * kTvlGaps);
@@ -374,7 +396,7 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
   const int CHY = TC * N;
 
   double pre[kDdPre];
-  double pre_nan = 0.0;
+  double pre_nan = 0.0, pre_sum[4] = {0.0, 0.0, 0.0, 0.0};
   auto load_chunk = [&](int c) {
     const size_t base = (size_t)c * CHY;
     const size_t lim = (size_t)T * N;
@@ -385,7 +407,10 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
       pre[q] = (e < CHY && g < lim) ? Y[g] : 0.0;
     }
     const int tc = c * TC + tid;
-    pre_nan = (tid < TC && tc < T) ? prep[(size_t)tc * ldp + np + 2] : 0.0;
+    const bool own = tid < TC && tc < T;
+    pre_nan = own ? prep[(size_t)tc * ldp + np + 2] : 0.0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) pre_sum[q] = own ? colsum[(size_t)tc * 4 + q] : 0.0;
   };
   auto store_chunk = [&]() {
 #pragma unroll
@@ -393,7 +418,11 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
       const int e = q * kDdBlock + tid;
       if (e < CHY) s_y[e] = pre[q];
     }
-    if (tid < TC) s_nan[tid] = pre_nan;
+    if (tid < TC) {
+      s_nan[tid] = pre_nan;
+      s_sum[2 * tid] = {pre_sum[0], pre_sum[1]};
+      s_sum[2 * tid + 1] = {pre_sum[2], pre_sum[3]};
+    }
   };
   if (nsteps > 0) {
     load_chunk(0);
@@ -430,30 +459,41 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
       const dd c2 = dd_mul(beta[2], dl);
       const dd k1 = dd_mul(c1, rl);
       const double* col = s_y + tt * N;
-      dd_acc S2, S3, S4, G22, G23, G24, G33, G34, G44, U1, U2, U3, U4, VV;
+      const dd kr = dd_mul(k1, rl);
+      // Per maturity only the loadings and their products with each other and with y, in the
+      // basis (z2, z, z4) — z3 = z2 − z is recovered per step below.  The innovation sums are
+      // recovered per step too: u = Z'y − Z'Z[:,1:3]β[1:3] and v'v = y'y − y'ŷ − ŷ'v, which in
+      // dd keeps ≥ 80 of 106 bits where the FP64 kernel (yfm_tvl.hip) forms v per maturity.
+      dd_acc S2, Sz, S4, G22, G2z, G24, Gzz, Gz4, G44, Y2, Yz, Y4;
       auto accum = [&](int i, dd z) {
         const double m = s_m[i];
-        const dd it = dd_mul(rl, s_rm[i]);                // 1/τ
+        const double y = col[i];
+        const dd rm = s_rm[i];
+        const dd it = dd_mul_nn(rl, rm);                     // 1/τ
         const dd z2 = dd_mul(dd_add_d(dd_neg(z), 1.0), it);  // (1 − z)/τ
-        const dd z3 = dd_sub(z2, z);
-        // ((β2+β3)(z/λ − z/(λ²m)) + β3·m·z)·(λ − 0.01) = z·(k1(1 − 1/τ·…) …): z·(k1(1 − it) + c2·m)
-        const dd z4 = dd_mul(z, dd_add(dd_mul(k1, dd_add_d(dd_neg(it), 1.0)), dd_mul_d(c2, m)));
-        const dd yh = dd_add(dd_add(beta[0], dd_mul(beta[1], z2)), dd_mul(beta[2], z3));
-        const dd v = dd_add_d(dd_neg(yh), col[i]);  // y − Z[:,1:3]β[1:3]
+        // ((β2+β3)(z/λ − z/(λ²m)) + β3·m·z)·(λ − 0.01) = z·t,  t = k1(1 − 1/τ) + c2·m
+        dd_acc ta;
+        ta.hi = k1.hi;
+        ta.lo = k1.lo;
+        ta.add(dd_mul_nn(dd_neg(kr), rm));
+        {
+          dd p = two_prod(c2.hi, m);
+          p.lo = __builtin_fma(c2.lo, m, p.lo);
+          ta.add(p);
+        }
+        const dd z4 = dd_mul_nn(z, ta.value());
         S2.add(z2);
-        S3.add(z3);
+        Sz.add(z);
         S4.add(z4);
         G22.add_prod(z2, z2);
-        G23.add_prod(z2, z3);
+        G2z.add_prod(z2, z);
         G24.add_prod(z2, z4);
-        G33.add_prod(z3, z3);
-        G34.add_prod(z3, z4);
+        Gzz.add_prod(z, z);
+        Gz4.add_prod(z, z4);
         G44.add_prod(z4, z4);
-        U1.add(v);
-        U2.add_prod(z2, v);
-        U3.add_prod(z3, v);
-        U4.add_prod(z4, v);
-        VV.add_prod(v, v);
+        Y2.add_prod_d(z2, y);
+        Yz.add_prod_d(z, y);
+        Y4.add_prod_d(z4, y);
       };
       if (K > 0) {
         dd* w = s_w + grp * kTvlGaps;
@@ -470,19 +510,47 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
       } else {
         for (int i = j; i < N; i += L) accum(i, dd_exp(dd_neg(dd_mul_d(lam, s_m[i]))));
       }
+      const dd s2 = group_sum_acc<L>(S2), sz = group_sum_acc<L>(Sz), s4 = group_sum_acc<L>(S4);
+      const dd g22 = group_sum_acc<L>(G22), g2z = group_sum_acc<L>(G2z), g24 = group_sum_acc<L>(G24);
+      const dd gzz = group_sum_acc<L>(Gzz), gz4 = group_sum_acc<L>(Gz4), g44 = group_sum_acc<L>(G44);
+      const dd y2 = group_sum_acc<L>(Y2), yz = group_sum_acc<L>(Yz), y4 = group_sum_acc<L>(Y4);
+      // back to the loading basis (1, z2, z3 = z2 − z, z4)
+      const dd g23 = dd_sub(g22, g2z);
       dd G[M4][M4];
       G[0][0] = dd_make((double)N);
-      G[0][1] = G[1][0] = group_sum_acc<L>(S2);
-      G[0][2] = G[2][0] = group_sum_acc<L>(S3);
-      G[0][3] = G[3][0] = group_sum_acc<L>(S4);
-      G[1][1] = group_sum_acc<L>(G22);
-      G[1][2] = G[2][1] = group_sum_acc<L>(G23);
-      G[1][3] = G[3][1] = group_sum_acc<L>(G24);
-      G[2][2] = group_sum_acc<L>(G33);
-      G[2][3] = G[3][2] = group_sum_acc<L>(G34);
-      G[3][3] = group_sum_acc<L>(G44);
-      const dd u[M4] = {group_sum_acc<L>(U1), group_sum_acc<L>(U2), group_sum_acc<L>(U3), group_sum_acc<L>(U4)};
-      const dd vv = group_sum_acc<L>(VV);
+      G[0][1] = G[1][0] = s2;
+      G[0][2] = G[2][0] = dd_sub(s2, sz);
+      G[0][3] = G[3][0] = s4;
+      G[1][1] = g22;
+      G[1][2] = G[2][1] = g23;
+      G[1][3] = G[3][1] = g24;
+      G[2][2] = dd_add(dd_sub(g23, g2z), gzz);  // Σ(z2 − z)² = g22 − 2 g2z + gzz
+      G[2][3] = G[3][2] = dd_sub(g24, gz4);
+      G[3][3] = g44;
+      const dd y3 = dd_sub(y2, yz);
+      // u_c = Σ_i Z_ic (y_i − ŷ_i), ŷ = β1 + β2 z2 + β3 z3;  v'v = y'y − β'(Z'y)[1:3] − β'u[1:3]
+      const dd sy = s_sum[2 * tt], syy = s_sum[2 * tt + 1];
+      const dd zy[M4] = {sy, y2, y3, y4};
+      dd u[M4];
+#pragma unroll
+      for (int c = 0; c < M4; ++c) {
+        dd_acc a;
+        a.add(zy[c]);
+#pragma unroll
+        for (int l = 0; l < 3; ++l) a.add_prod(dd_neg(beta[l]), G[c][l]);
+        u[c] = a.value();
+      }
+      dd vv;
+      {
+        dd_acc a;
+        a.add(syy);
+#pragma unroll
+        for (int l = 0; l < 3; ++l) {
+          a.add_prod(dd_neg(beta[l]), zy[l]);
+          a.add_prod(dd_neg(beta[l]), u[l]);
+        }
+        vv = a.value();
+      }
 
       // ---- capacitance solve: B̃ = σ²I + P G, W = B̃⁻¹P ----
       dd A[M4][M4], W[M4][M4];
@@ -580,7 +648,7 @@ template <int L>
 hipError_t launch_tvl_dd_l(const LaunchArgs& a, const double* rec_dd, const TvlGaps& g, int TC) {
   constexpr int GPB = kDdBlock / L;
   const int grid = (a.B + GPB - 1) / GPB;
-  const size_t shmem = sizeof(double) * (size_t)(3 * a.N + TC + TC * a.N + GPB * kDPar + 2 * GPB * kTvlGaps) +
+  const size_t shmem = sizeof(double) * (size_t)(3 * a.N + 5 * TC + TC * a.N + GPB * kDPar + 2 * GPB * kTvlGaps) +
                        sizeof(int) * a.N;
   if (shmem > 160 * 1024) return hipErrorInvalidValue;  // gfx950: 160 KiB of LDS per workgroup
   auto* k = a.rec_beta ? &tvl_dd_loglik_kernel<L, true> : &tvl_dd_loglik_kernel<L, false>;
@@ -589,7 +657,9 @@ hipError_t launch_tvl_dd_l(const LaunchArgs& a, const double* rec_dd, const TvlG
                                        (int)shmem);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(k, dim3(grid), dim3(kDdBlock), shmem, a.stream, rec_dd, a.B, a.raw, a.panel, a.ldp, a.np, a.T,
+  const double* colsum = rec_dd + (size_t)kDRecLen * (size_t)(a.B > 0 ? a.B : 1);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kDdBlock), shmem, a.stream, rec_dd, a.B, a.raw, colsum, a.panel, a.ldp,
+                     a.np, a.T,
                      a.N, TC, a.mats, g.K, g.d, g.idx, a.T_use, a.out, a.flags, a.rec_beta, a.rec_P,
                      a.rec_beta ? a.horizon : 0, a.rec_beta ? a.rec_len : 0);
   return hipGetLastError();
@@ -597,7 +667,10 @@ hipError_t launch_tvl_dd_l(const LaunchArgs& a, const double* rec_dd, const TvlG
 
 }  // namespace
 
-size_t tvl_dd_scratch_bytes(int B) { return sizeof(double) * (size_t)kDRecLen * (size_t)(B > 0 ? B : 1); }
+// per-candidate records, then the panel's dd column sums (4 doubles per column)
+size_t tvl_dd_scratch_bytes(int B, int T) {
+  return sizeof(double) * ((size_t)kDRecLen * (size_t)(B > 0 ? B : 1) + 4 * (size_t)(T > 0 ? T : 1));
+}
 
 int tvl_dd_lanes_for(int B, int N, int want) {
   // one wave per SIMD of lanes (the kernel needs the whole 512-register file per lane), at
@@ -619,6 +692,8 @@ int tvl_dd_lanes_for(int B, int N, int want) {
 hipError_t launch_tvl_dd_init(const LaunchArgs& a, double* rec_dd) {
   hipLaunchKernelGGL(tvl_dd_init_kernel, dim3((a.B + 63) / 64), dim3(64), 0, a.stream, a.theta, a.P, a.B, a.space,
                      rec_dd);
+  hipLaunchKernelGGL(tvl_dd_colsum_kernel, dim3((a.T + 63) / 64), dim3(64), 0, a.stream, a.raw, a.N, a.T,
+                     rec_dd + (size_t)kDRecLen * (size_t)(a.B > 0 ? a.B : 1));
   return hipGetLastError();
 }
 
