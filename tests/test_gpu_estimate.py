@@ -149,3 +149,24 @@ def test_estimate_init_is_the_rescaled_start(engine, panel):
     r = engine.estimate(KIND_DNS, p[:, None], space=0, iterations=20, max_group_iters=1)
     assert r["status"][0] == 0 and np.isfinite(r["ll"][0])
     np.testing.assert_allclose(r["init_c"][:, 0], transform_params(KIND_DNS, q), rtol=1e-13)
+
+
+def test_speculation_is_bitwise_neutral(engine, panel):
+    """YFM_NM_SPEC=2 (two iterations per round, the default) vs 1 (one): the same chains bit for
+    bit and the same count of consumed evaluations, on 12 windows with rescaled and failing starts."""
+    import os
+    Y, mats = panel
+    engine.set_panel(Y, mats)
+    starts = S.theta_batch(KIND_DNS, 12, seed=67, bad_frac=0.2, scale=0.08)
+    win = np.array([80, 79, 70, 66, 60, 55, 50, 45, 40, 33, 80, 72], dtype=np.int32)
+    res = {}
+    for mode in ("1", "2"):
+        os.environ["YFM_NM_SPEC"] = mode
+        try:
+            res[mode] = engine.estimate(KIND_DNS, starts, space=0, T_use=win, iterations=200, max_group_iters=3)
+        finally:
+            os.environ.pop("YFM_NM_SPEC", None)
+    a, b = res["1"], res["2"]
+    for k in ("theta_c", "p", "init_c", "ll", "status"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    assert a["n_evals"] == b["n_evals"]

@@ -23,12 +23,25 @@
 // reference's branch (unused values are discarded, including their failures).  A shrink
 // costs one extra round.  The arithmetic of the simplex updates follows Optim's
 // operation order with FP contraction off, so the chain is bitwise reproducible.
+//
+// Two-iteration speculation (YFM_NM_SPEC=2, the default): the round that evaluates an
+// iteration's four trial points also evaluates the next iteration's four for each way this
+// one can end without a shrink â€” the accepted point (reflection, expansion, outside or
+// inside contraction) and whether it becomes the new worst vertex (only a contraction can):
+// six simplices, 24 more points.  After the real outcome is known, the chain's next trial
+// points are those of exactly one speculated simplex (same vertices, same worst index, so
+// the same arithmetic); its values are consumed at once and the iteration costs no round.
+// The chain's sequence of states, and so its result, is bitwise that of one iteration per
+// round; n_evals counts the evaluations the chain consumed (as without speculation).
 #pragma clang fp contract(off)
 
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <vector>
@@ -110,6 +123,16 @@ struct Chain {
   std::vector<double> xc, xl, trial;  // centroid, best vertex, requested points
   int n_req = 0;
   size_t req_off = 0;
+  // speculation: the next iteration's trial points for each non-shrink outcome of this one
+  struct Spec {
+    int src;  // accepted trial point: 0 reflection, 1 expansion, 2 outside, 3 inside contraction
+    int hp;   // the worst vertex after the update
+  };
+  std::vector<Spec> spec;
+  std::vector<double> spec_pts;  // 4n per entry of spec, in request order after the 4 real points
+  int acc_src = -1;              // accepted trial point of the last NM_ITER consume (-1: shrink)
+  long long used = 0;            // evaluations consumed by the chain
+  long long spec_hits = 0;
 };
 
 void sortperm(Chain& c) {
@@ -156,10 +179,28 @@ Params nm_parameters(int n) {  // Optim.AdaptiveParameters: (Î±, Î² + 2/n, Î³ âˆ
   return {1.0, 1.0 + 2.0 / n, 0.75 - 1.0 / (2.0 * n), 1.0 - 1.0 / n};
 }
 
+// Nelderâ€“Mead trial points of the iteration whose worst vertex is h: centroid of the other
+// vertices (storage order), then reflection, expansion, outside and inside contraction
+void iter_trials(const Chain& c, int h, double* xc, double* trial) {
+  const int n = c.n;
+  const Params q = nm_parameters(n);
+  centroid(c, h, xc);
+  const double* xh = &c.S[(size_t)h * n];
+  double* xr = trial;
+  for (int k = 0; k < n; ++k) xr[k] = xc[k] + q.al * (xc[k] - xh[k]);
+  for (int k = 0; k < n; ++k) {
+    const double d = xr[k] - xc[k];
+    trial[n + k] = xc[k] + q.be * d;      // expansion
+    trial[2 * n + k] = xc[k] + q.ga * d;  // outside contraction
+    trial[3 * n + k] = xc[k] - q.ga * d;  // inside contraction
+  }
+}
+
 // Queue the points chain c needs this round; advances phases that need no evaluation.
-void prepare(Chain& c, int iterations, std::vector<double>& batch, std::vector<int>& tuse) {
+void prepare(Chain& c, int iterations, int spec_depth, std::vector<double>& batch, std::vector<int>& tuse) {
   const int n = c.n, m = n + 1;
   c.n_req = 0;
+  c.spec.clear();
   if (c.phase == NM_ITER && (c.converged || c.it >= iterations)) c.phase = NM_FINAL;
   c.trial.clear();
   switch (c.phase) {
@@ -181,18 +222,22 @@ void prepare(Chain& c, int iterations, std::vector<double>& batch, std::vector<i
       break;
     }
     case NM_ITER: {
-      const Params q = nm_parameters(n);
       c.xc.assign(n, 0.0);
-      centroid(c, c.order[m - 1], c.xc.data());
-      const double* xh = &c.S[(size_t)c.order[m - 1] * n];
       c.trial.assign((size_t)4 * n, 0.0);
-      double* xr = &c.trial[0];
-      for (int k = 0; k < n; ++k) xr[k] = c.xc[k] + q.al * (c.xc[k] - xh[k]);
-      for (int k = 0; k < n; ++k) {
-        const double d = xr[k] - c.xc[k];
-        c.trial[n + k] = c.xc[k] + q.be * d;          // expansion
-        c.trial[2 * n + k] = c.xc[k] + q.ga * d;      // outside contraction
-        c.trial[3 * n + k] = c.xc[k] - q.ga * d;      // inside contraction
+      iter_trials(c, c.order[m - 1], c.xc.data(), c.trial.data());
+      if (spec_depth >= 2) {
+        // the six simplices the next iteration can start from (see the file header)
+        static const Chain::Spec kinds[6] = {{0, 0}, {1, 0}, {2, 0}, {2, 1}, {3, 0}, {3, 1}};
+        const int ih = c.order[m - 1], ish = c.order[m - 2];
+        c.spec_pts.assign((size_t)6 * 4 * n, 0.0);
+        std::vector<double> xc2(n), saved(c.S.begin() + (size_t)ih * n, c.S.begin() + (size_t)(ih + 1) * n);
+        for (int k = 0; k < 6; ++k) {
+          const int src = kinds[k].src, hp = kinds[k].hp ? ih : ish;
+          c.spec.push_back({src, hp});
+          std::copy(&c.trial[(size_t)src * n], &c.trial[(size_t)(src + 1) * n], c.S.begin() + (size_t)ih * n);
+          iter_trials(c, hp, xc2.data(), &c.spec_pts[(size_t)k * 4 * n]);
+        }
+        std::copy(saved.begin(), saved.end(), c.S.begin() + (size_t)ih * n);
       }
       break;
     }
@@ -219,7 +264,8 @@ void prepare(Chain& c, int iterations, std::vector<double>& batch, std::vector<i
   c.n_req = (int)(c.trial.size() / n);
   c.req_off = batch.size() / n;
   batch.insert(batch.end(), c.trial.begin(), c.trial.end());
-  tuse.insert(tuse.end(), c.n_req, c.window);
+  batch.insert(batch.end(), c.spec_pts.begin(), c.spec_pts.begin() + (size_t)c.spec.size() * 4 * n);
+  tuse.insert(tuse.end(), c.n_req + 4 * c.spec.size(), c.window);
 }
 
 // objective values âˆ’loglik of this chain's requests; NaN â‡” compute_loss threw
@@ -260,6 +306,7 @@ void consume(Chain& c, const double* f, int max_group_iters, double tol, double 
       return;
     case NM_ITER: {
       ++c.it;
+      c.acc_src = -1;
       const int il = c.order[0], ish = c.order[n - 1], ih = c.order[m - 1];
       const double fl = c.fs[il], fsh = c.fs[ish], fh = c.fs[ih];
       c.xl.assign(c.S.begin() + (size_t)il * n, c.S.begin() + (size_t)(il + 1) * n);
@@ -274,15 +321,18 @@ void consume(Chain& c, const double* f, int max_group_iters, double tol, double 
         if (fe < fr) {
           std::copy(&c.trial[n], &c.trial[2 * n], xh);
           c.fs[ih] = fe;
+          c.acc_src = 1;
         } else {
           std::copy(xr, xr + n, xh);
           c.fs[ih] = fr;
+          c.acc_src = 0;
         }
         for (int i = m - 1; i >= 1; --i) c.order[i] = c.order[i - 1];  // the new vertex is the lowest
         c.order[0] = ih;
       } else if (fr < fsh) {
         std::copy(xr, xr + n, xh);
         c.fs[ih] = fr;
+        c.acc_src = 0;
         sortperm(c);
       } else if (fr < fh) {
         const double fo = f[2];
@@ -290,6 +340,7 @@ void consume(Chain& c, const double* f, int max_group_iters, double tol, double 
         if (fo < fr) {
           std::copy(&c.trial[2 * n], &c.trial[3 * n], xh);
           c.fs[ih] = fo;
+          c.acc_src = 2;
           sortperm(c);
         } else {
           shrink = true;
@@ -300,6 +351,7 @@ void consume(Chain& c, const double* f, int max_group_iters, double tol, double 
         if (fi < fh) {
           std::copy(&c.trial[3 * n], &c.trial[4 * n], xh);
           c.fs[ih] = fi;
+          c.acc_src = 3;
           sortperm(c);
         } else {
           shrink = true;
@@ -384,14 +436,20 @@ extern "C" int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const
       c.p[i] = std::isfinite(x) ? x : 0.0;  // _sanitize_parameters (optimization.jl:422-432)
     }
   }
+  int spec_depth = 2;
+  if (const char* e = std::getenv("YFM_NM_SPEC")) spec_depth = std::atoi(e);
+  const bool stats = std::getenv("YFM_EST_STATS") != nullptr;
   std::vector<double> batch, out;
   std::vector<int> tuse;
   PinnedBuf pin_th, pin_tu, pin_out;
-  long long evals = 0;
+  long long evals = 0, device_evals = 0, rounds = 0;
+  double t_host = 0.0, t_dev = 0.0;
+  using clk = std::chrono::steady_clock;
   for (;;) {
+    const auto t0 = clk::now();
     batch.clear();
     tuse.clear();
-    for (Chain& c : chains) prepare(c, iterations, batch, tuse);
+    for (Chain& c : chains) prepare(c, iterations, spec_depth, batch, tuse);
     const int B = (int)(batch.size() / P);
     if (B == 0) break;
     out.resize(B);
@@ -401,16 +459,50 @@ extern "C" int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const
       return yfm::api_error(YFM_EHIP, "hipHostMalloc failed for the estimation batch");
     std::memcpy(pin_th.p, batch.data(), sizeof(double) * batch.size());
     if (T_use) std::memcpy(pin_tu.p, tuse.data(), sizeof(int) * (size_t)B);
+    const auto t1 = clk::now();
     const int rc = yfm_loglik_batch(ctx, model_kind, YFM_THETA_UNCONSTRAINED, static_cast<const double*>(pin_th.p),
                                     P, B, T_use ? static_cast<const int*>(pin_tu.p) : nullptr,
                                     static_cast<double*>(pin_out.p));
     if (rc != YFM_OK) return rc;
+    const auto t2 = clk::now();
     std::memcpy(out.data(), pin_out.p, sizeof(double) * (size_t)B);
-    evals += B;
+    device_evals += B;
+    ++rounds;
     for (double& v : out) v = -v;  // compute_loss = âˆ’loglik (optimization.jl:22)
-    for (Chain& c : chains)
-      if (c.n_req > 0) consume(c, out.data() + c.req_off, max_group_iters, tol, g_tol);
+    for (Chain& c : chains) {
+      if (c.n_req == 0) continue;
+      const double* f = out.data() + c.req_off;
+      consume(c, f, max_group_iters, tol, g_tol);
+      c.used += c.n_req;
+      // a speculated next iteration whose simplex is the one the chain now holds
+      if (c.phase == NM_ITER && c.acc_src >= 0 && !c.converged && c.it < iterations) {
+        const int hp = c.order[c.n];
+        for (size_t k = 0; k < c.spec.size(); ++k) {
+          if (c.spec[k].src != c.acc_src || c.spec[k].hp != hp) continue;
+          const size_t w = (size_t)4 * c.n;
+          c.trial.assign(c.spec_pts.begin() + k * w, c.spec_pts.begin() + (k + 1) * w);
+          c.spec.clear();
+          consume(c, f + 4 + 4 * k, max_group_iters, tol, g_tol);
+          c.used += 4;
+          ++c.spec_hits;
+          break;
+        }
+      }
+      c.spec.clear();
+    }
+    const auto t3 = clk::now();
+    t_host += std::chrono::duration<double>((t1 - t0) + (t3 - t2)).count();
+    t_dev += std::chrono::duration<double>(t2 - t1).count();
   }
+  long long hits = 0;
+  for (const Chain& c : chains) {
+    evals += c.used;
+    hits += c.spec_hits;
+  }
+  if (stats)
+    std::fprintf(stderr, "yfm_estimate: %lld rounds, %lld chain evaluations, %lld device evaluations, %lld "
+                 "speculated iterations used; host %.3f s, loglik calls %.3f s\n", rounds, evals, device_evals,
+                 hits, t_host, t_dev);
   for (int r = 0; r < R; ++r) {
     const Chain& c = chains[r];
     const bool ok = c.status != 1;
