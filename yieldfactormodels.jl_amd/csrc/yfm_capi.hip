@@ -326,6 +326,7 @@ int validate_tuse(const int* T_use, int B, int T) {
 
 namespace yfm {
 int api_error(int code, const char* msg) { return set_error(code, "%s", msg); }
+int panel_T(const yfm_ctx* ctx) { return ctx ? ctx->T : 0; }
 }  // namespace yfm
 
 extern "C" {

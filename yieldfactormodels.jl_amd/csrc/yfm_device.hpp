@@ -398,19 +398,26 @@ struct LDLT {
 // `phi(i, j)` returns Φ_ij (registers, or LDS for the 5-factor kernel); each row of Φ is
 // read once per product so an LDS-backed Φ costs 2·M² reads per step.
 template <int M, class PhiF>
-__device__ __forceinline__ void propagate_state_f(PhiF phi, const double (&Q)[M][M], const double (&delta)[M],
-                                                  const double (&bf)[M], const double (&Pf)[M][M], double (&beta)[M],
-                                                  double (&Pm)[M][M]) {
+__device__ __forceinline__ void propagate_mean_f(PhiF phi, const double (&delta)[M], const double (&bf)[M],
+                                                 double (&beta)[M]) {
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    double s = delta[i];
+#pragma unroll
+    for (int j = 0; j < M; ++j) s = fma(phi(i, j), bf[j], s);
+    beta[i] = s;
+  }
+}
+
+template <int M, class PhiF>
+__device__ __forceinline__ void propagate_cov_f(PhiF phi, const double (&Q)[M][M], const double (&Pf)[M][M],
+                                                double (&Pm)[M][M]) {
   double A[M][M];
 #pragma unroll
   for (int i = 0; i < M; ++i) {
     double f[M];
 #pragma unroll
     for (int j = 0; j < M; ++j) f[j] = phi(i, j);
-    double s = delta[i];
-#pragma unroll
-    for (int j = 0; j < M; ++j) s = fma(f[j], bf[j], s);
-    beta[i] = s;
 #pragma unroll
     for (int j = 0; j < M; ++j) {
       double a = 0.0;
@@ -433,6 +440,14 @@ __device__ __forceinline__ void propagate_state_f(PhiF phi, const double (&Q)[M]
       Pm[j][i] = s;
     }
   }
+}
+
+template <int M, class PhiF>
+__device__ __forceinline__ void propagate_state_f(PhiF phi, const double (&Q)[M][M], const double (&delta)[M],
+                                                  const double (&bf)[M], const double (&Pf)[M][M], double (&beta)[M],
+                                                  double (&Pm)[M][M]) {
+  propagate_mean_f<M>(phi, delta, bf, beta);
+  propagate_cov_f<M>(phi, Q, Pf, Pm);
 }
 
 template <int M, int LEAD>

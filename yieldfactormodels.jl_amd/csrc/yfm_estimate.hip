@@ -38,7 +38,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <thread>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -72,6 +77,8 @@ struct PinnedBuf {
 };
 
 enum Code { ID = 0, POS = 1, R11 = 2 };
+
+constexpr int kMaxSlot = 128;  // points per chain and round (≥ P + 1)
 
 // transform vectors: kalmanbasemodel.jl:74-120 (+ dns.jl:15-22 one leading γ; GNS5 two)
 std::vector<int> transform_codes(int kind) {
@@ -122,7 +129,6 @@ struct Chain {
   bool converged = false;
   std::vector<double> xc, xl, trial;  // centroid, best vertex, requested points
   int n_req = 0;
-  size_t req_off = 0;
   // speculation: the next iteration's trial points for each non-shrink outcome of this one
   struct Spec {
     int src;  // accepted trial point: 0 reflection, 1 expansion, 2 outside, 3 inside contraction
@@ -130,6 +136,7 @@ struct Chain {
   };
   std::vector<Spec> spec;
   std::vector<double> spec_pts;  // 4n per entry of spec, in request order after the 4 real points
+  std::vector<double> tmp;       // scratch of the speculation (centroid, saved vertex)
   int acc_src = -1;              // accepted trial point of the last NM_ITER consume (-1: shrink)
   long long used = 0;            // evaluations consumed by the chain
   long long spec_hits = 0;
@@ -197,7 +204,7 @@ void iter_trials(const Chain& c, int h, double* xc, double* trial) {
 }
 
 // Queue the points chain c needs this round; advances phases that need no evaluation.
-void prepare(Chain& c, int iterations, int spec_depth, std::vector<double>& batch, std::vector<int>& tuse) {
+void prepare(Chain& c, int iterations, int spec_depth) {
   const int n = c.n, m = n + 1;
   c.n_req = 0;
   c.spec.clear();
@@ -229,15 +236,19 @@ void prepare(Chain& c, int iterations, int spec_depth, std::vector<double>& batc
         // the six simplices the next iteration can start from (see the file header)
         static const Chain::Spec kinds[6] = {{0, 0}, {1, 0}, {2, 0}, {2, 1}, {3, 0}, {3, 1}};
         const int ih = c.order[m - 1], ish = c.order[m - 2];
-        c.spec_pts.assign((size_t)6 * 4 * n, 0.0);
-        std::vector<double> xc2(n), saved(c.S.begin() + (size_t)ih * n, c.S.begin() + (size_t)(ih + 1) * n);
+        c.spec_pts.resize((size_t)6 * 4 * n);
+        c.tmp.resize((size_t)2 * n);
+        double* xc2 = c.tmp.data();
+        double* saved = xc2 + n;
+        double* vh = &c.S[(size_t)ih * n];
+        std::copy(vh, vh + n, saved);
         for (int k = 0; k < 6; ++k) {
           const int src = kinds[k].src, hp = kinds[k].hp ? ih : ish;
           c.spec.push_back({src, hp});
-          std::copy(&c.trial[(size_t)src * n], &c.trial[(size_t)(src + 1) * n], c.S.begin() + (size_t)ih * n);
-          iter_trials(c, hp, xc2.data(), &c.spec_pts[(size_t)k * 4 * n]);
+          std::copy(&c.trial[(size_t)src * n], &c.trial[(size_t)(src + 1) * n], vh);
+          iter_trials(c, hp, xc2, &c.spec_pts[(size_t)k * 4 * n]);
         }
-        std::copy(saved.begin(), saved.end(), c.S.begin() + (size_t)ih * n);
+        std::copy(saved, saved + n, vh);
       }
       break;
     }
@@ -262,11 +273,75 @@ void prepare(Chain& c, int iterations, int spec_depth, std::vector<double>& batc
       return;
   }
   c.n_req = (int)(c.trial.size() / n);
-  c.req_off = batch.size() / n;
-  batch.insert(batch.end(), c.trial.begin(), c.trial.end());
-  batch.insert(batch.end(), c.spec_pts.begin(), c.spec_pts.begin() + (size_t)c.spec.size() * 4 * n);
-  tuse.insert(tuse.end(), c.n_req + 4 * c.spec.size(), c.window);
 }
+
+// Minimal fork-join pool for the per-round host work (chains are independent).
+class Pool {
+ public:
+  explicit Pool(int n) {
+    for (int i = 1; i < n; ++i) th_.emplace_back([this] { worker(); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  // f(i) for i in [0, n), items handed out in chunks; returns when all are done
+  template <class F>
+  void run(int n, int chunk, F&& f) {
+    if (th_.empty() || n <= chunk) {
+      for (int i = 0; i < n; ++i) f(i);
+      return;
+    }
+    std::function<void(int)> job = [&](int i) { f(i); };
+    {
+      std::lock_guard<std::mutex> g(m_);
+      job_ = &job;
+      n_ = n;
+      chunk_ = chunk;
+      next_.store(0);
+      done_.store(0);
+      ++gen_;
+    }
+    cv_.notify_all();
+    drain();
+    while (done_.load(std::memory_order_acquire) < n) std::this_thread::yield();
+    std::lock_guard<std::mutex> g(m_);
+    job_ = nullptr;
+  }
+
+ private:
+  void drain() {
+    for (;;) {
+      const int i0 = next_.fetch_add(chunk_);
+      if (i0 >= n_) return;
+      const int i1 = std::min(n_, i0 + chunk_);
+      for (int i = i0; i < i1; ++i) (*job_)(i);
+      done_.fetch_add(i1 - i0, std::memory_order_release);
+    }
+  }
+  void worker() {
+    int seen = 0;
+    for (;;) {
+      std::unique_lock<std::mutex> lk(m_);
+      cv_.wait(lk, [&] { return stop_ || (gen_ != seen && job_); });
+      if (stop_) return;
+      seen = gen_;
+      lk.unlock();
+      drain();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::function<void(int)>* job_ = nullptr;
+  int n_ = 0, chunk_ = 1, gen_ = 0;
+  bool stop_ = false;
+  std::atomic<int> next_{0}, done_{0};
+};
 
 // objective values −loglik of this chain's requests; NaN ⇔ compute_loss threw
 void fail(Chain& c) {
@@ -423,6 +498,11 @@ extern "C" int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const
     return yfm::api_error(YFM_EINVAL, "R, iterations must be >= 0 and max_group_iters >= 1");
   if (R == 0) return YFM_OK;
   if (!theta0 || !theta_c_out || !ll_out) return yfm::api_error(YFM_EINVAL, "null pointer argument");
+  const int Tp = yfm::panel_T(ctx);
+  if (Tp <= 0) return yfm::api_error(YFM_ENOPANEL, "no panel: call yfm_set_panel first");
+  if (T_use)
+    for (int r = 0; r < R; ++r)
+      if (T_use[r] < 1 || T_use[r] > Tp) return yfm::api_error(YFM_EINVAL, "T_use outside [1, T]");
   const std::vector<int> codes = transform_codes(model_kind);
   std::vector<Chain> chains(R);
   for (int r = 0; r < R; ++r) {
@@ -439,39 +519,60 @@ extern "C" int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const
   int spec_depth = 2;
   if (const char* e = std::getenv("YFM_NM_SPEC")) spec_depth = std::atoi(e);
   const bool stats = std::getenv("YFM_EST_STATS") != nullptr;
-  std::vector<double> batch, out;
-  std::vector<int> tuse;
+  // Every chain owns a fixed slot of SLOT points in the round's batch (its requests, then its
+  // speculated points; the rest of the slot keeps earlier values and its results are ignored),
+  // so each chain's host work — consume the last results, prepare, write the slot — runs in
+  // parallel, straight into page-locked memory, and T_use is written once.
+  const int SLOT = std::max(spec_depth >= 2 ? 28 : 4, P + 1);
+  if (SLOT > kMaxSlot) return yfm::api_error(YFM_EINVAL, "too many parameters for the estimation driver");
+  const int B = R * SLOT;
   PinnedBuf pin_th, pin_tu, pin_out;
-  long long evals = 0, device_evals = 0, rounds = 0;
+  if (pin_th.ensure(sizeof(double) * (size_t)B * P) != hipSuccess ||
+      pin_out.ensure(sizeof(double) * (size_t)B) != hipSuccess ||
+      (T_use && pin_tu.ensure(sizeof(int) * (size_t)B) != hipSuccess))
+    return yfm::api_error(YFM_EHIP, "hipHostMalloc failed for the estimation batch");
+  double* th = static_cast<double*>(pin_th.p);
+  double* out = static_cast<double*>(pin_out.p);
+  std::memset(th, 0, sizeof(double) * (size_t)B * P);
+  if (T_use)
+    for (int r = 0; r < R; ++r) std::fill_n(static_cast<int*>(pin_tu.p) + (size_t)r * SLOT, SLOT, T_use[r]);
+  // device-side batch: θ uploaded per round on this call's own stream, T_use once
+  hipStream_t st = nullptr;
+  double *d_th = nullptr, *d_out = nullptr;
+  int* d_tu = nullptr;
+  struct Release {
+    hipStream_t& s;
+    double*& a;
+    double*& b;
+    int*& c;
+    ~Release() {
+      if (s) (void)hipStreamSynchronize(s);
+      if (a) (void)hipFree(a);
+      if (b) (void)hipFree(b);
+      if (c) (void)hipFree(c);
+      if (s) (void)hipStreamDestroy(s);
+    }
+  } release{st, d_th, d_out, d_tu};
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc(&d_th, sizeof(double) * (size_t)B * P) != hipSuccess ||
+      hipMalloc(&d_out, sizeof(double) * (size_t)B) != hipSuccess ||
+      (T_use && hipMalloc(&d_tu, sizeof(int) * (size_t)B) != hipSuccess))
+    return yfm::api_error(YFM_EHIP, "device allocation failed for the estimation batch");
+  if (T_use && hipMemcpy(d_tu, pin_tu.p, sizeof(int) * (size_t)B, hipMemcpyHostToDevice) != hipSuccess)
+    return yfm::api_error(YFM_EHIP, "T_use upload failed");
+  int nthreads = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+  if (const char* e = std::getenv("YFM_EST_THREADS")) nthreads = std::max(1, std::atoi(e));
+  Pool pool(std::min(nthreads, std::max(1, R / 16)));
+  std::atomic<int> active{0};
+  long long device_evals = 0, rounds = 0;
   double t_host = 0.0, t_dev = 0.0;
   using clk = std::chrono::steady_clock;
-  for (;;) {
-    const auto t0 = clk::now();
-    batch.clear();
-    tuse.clear();
-    for (Chain& c : chains) prepare(c, iterations, spec_depth, batch, tuse);
-    const int B = (int)(batch.size() / P);
-    if (B == 0) break;
-    out.resize(B);
-    if (pin_th.ensure(sizeof(double) * batch.size()) != hipSuccess ||
-        pin_out.ensure(sizeof(double) * (size_t)B) != hipSuccess ||
-        (T_use && pin_tu.ensure(sizeof(int) * (size_t)B) != hipSuccess))
-      return yfm::api_error(YFM_EHIP, "hipHostMalloc failed for the estimation batch");
-    std::memcpy(pin_th.p, batch.data(), sizeof(double) * batch.size());
-    if (T_use) std::memcpy(pin_tu.p, tuse.data(), sizeof(int) * (size_t)B);
-    const auto t1 = clk::now();
-    const int rc = yfm_loglik_batch(ctx, model_kind, YFM_THETA_UNCONSTRAINED, static_cast<const double*>(pin_th.p),
-                                    P, B, T_use ? static_cast<const int*>(pin_tu.p) : nullptr,
-                                    static_cast<double*>(pin_out.p));
-    if (rc != YFM_OK) return rc;
-    const auto t2 = clk::now();
-    std::memcpy(out.data(), pin_out.p, sizeof(double) * (size_t)B);
-    device_evals += B;
-    ++rounds;
-    for (double& v : out) v = -v;  // compute_loss = −loglik (optimization.jl:22)
-    for (Chain& c : chains) {
-      if (c.n_req == 0) continue;
-      const double* f = out.data() + c.req_off;
+  auto host_step = [&](int r) {
+    Chain& c = chains[r];
+    if (c.n_req > 0) {  // the results of this chain's slot from the last round
+      double f[kMaxSlot];
+      const int nv = c.n_req + 4 * (int)c.spec.size();
+      for (int k = 0; k < nv; ++k) f[k] = -out[(size_t)r * SLOT + k];  // compute_loss = −loglik (optimization.jl:22)
       consume(c, f, max_group_iters, tol, g_tol);
       c.used += c.n_req;
       // a speculated next iteration whose simplex is the one the chain now holds
@@ -490,10 +591,34 @@ extern "C" int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const
       }
       c.spec.clear();
     }
-    const auto t3 = clk::now();
-    t_host += std::chrono::duration<double>((t1 - t0) + (t3 - t2)).count();
+    prepare(c, iterations, spec_depth);
+    if (c.n_req == 0) return;
+    active.fetch_add(1, std::memory_order_relaxed);
+    double* slot = th + (size_t)r * SLOT * P;
+    std::memcpy(slot, c.trial.data(), sizeof(double) * c.trial.size());
+    if (!c.spec.empty())
+      std::memcpy(slot + c.trial.size(), c.spec_pts.data(), sizeof(double) * c.spec.size() * 4 * (size_t)P);
+  };
+  for (;;) {
+    const auto t0 = clk::now();
+    active.store(0);
+    pool.run(R, 8, host_step);
+    if (active.load() == 0) break;
+    const auto t1 = clk::now();
+    if (hipMemcpyAsync(d_th, th, sizeof(double) * (size_t)B * P, hipMemcpyHostToDevice, st) != hipSuccess)
+      return yfm::api_error(YFM_EHIP, "θ upload failed");
+    const int rc = yfm_loglik_batch_device(ctx, model_kind, YFM_THETA_UNCONSTRAINED, d_th, P, B, d_tu, d_out, st);
+    if (rc != YFM_OK) return rc;
+    if (hipMemcpyAsync(out, d_out, sizeof(double) * (size_t)B, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return yfm::api_error(YFM_EHIP, "loglik download failed");
+    const auto t2 = clk::now();
+    device_evals += B;
+    ++rounds;
+    t_host += std::chrono::duration<double>(t1 - t0).count();
     t_dev += std::chrono::duration<double>(t2 - t1).count();
   }
+  long long evals = 0;
   long long hits = 0;
   for (const Chain& c : chains) {
     evals += c.used;

@@ -6,6 +6,10 @@
 // Restates filter.jl:125-179 (filter!), :182-209 (get_loss) and :1-10 (initialize_filter)
 // in the collapsed form of DESIGN.md §3.1 (see yfm_kernels.hip's header).
 #pragma once
+// No implicit FMA contraction in the fixed-loading kernels: every fused multiply-add is an
+// explicit fma(), so the kernels that share this code (the per-lane and the lane-group
+// kernel) round identically wherever it is inlined, whatever the surrounding code.
+#pragma clang fp contract(off)
 #include "yfm_device.hpp"
 
 namespace yfm {

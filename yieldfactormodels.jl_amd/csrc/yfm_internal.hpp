@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "../../include/yfm.h"
+
 namespace yfm {
 
 struct LaunchArgs {
@@ -81,6 +83,8 @@ hipError_t launch_forecast_emit(const PredictArgs& a);
 hipError_t launch_loss_array(const PredictArgs& a, const double* Y, int T1, int passes, unsigned int* flags);
 // record `msg` as yfm_last_error() for this thread and return `code` (host helpers above the C ABI)
 int api_error(int code, const char* msg);
+// columns of the context's panel (0 before yfm_set_panel)
+int panel_T(const yfm_ctx* ctx);
 hipError_t launch_prep_panel(const double* Y, int N, int T, int np, int ldp, double* out, hipStream_t s);
 
 }  // namespace yfm

@@ -34,6 +34,9 @@ namespace {
 constexpr int kDdBlock = 256;
 constexpr int kDdPre = 8;  // panel doubles prefetched per thread per chunk
 constexpr int M4 = 4;
+// per-group jump factors e^{−λ d_k} in LDS: 9 dd (144 B) apart, so the 16 groups of a wave
+// reading their own table hit disjoint banks (a 128 B stride is a 4-way conflict)
+constexpr int kDdWStride = kTvlGaps + 1;
 
 // per-candidate record written by tvl_dd_init_kernel (doubles)
 constexpr int kDSig = 0;     // σ² (dd)
@@ -349,7 +352,7 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
   double* s_y = s_nan + 5 * TC;                        // TC columns of N yields
   double* s_par = s_y + TC * N;                        // per group: σ², δ, Φ, Q (kDPar doubles)
   dd* s_w = reinterpret_cast<dd*>(s_par + GPB * kDPar);  // per group: e^{-λ d_k}, k < K
-  int* s_gi = reinterpret_cast<int*>(s_w + GPB * kTvlGaps);
+  int* s_gi = reinterpret_cast<int*>(s_w + GPB * kDdWStride);
   __shared__ double s_gd[kTvlGaps];
   __shared__ int s_nobs_max;
 
@@ -496,7 +499,7 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
         Y4.add_prod_d(z4, y);
       };
       if (K > 0) {
-        dd* w = s_w + grp * kTvlGaps;
+        dd* w = s_w + grp * kDdWStride;
         for (int q = j; q < K; q += L) w[q] = dd_exp(dd_neg(dd_mul_d(lam, s_gd[q])));
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -648,7 +651,7 @@ template <int L>
 hipError_t launch_tvl_dd_l(const LaunchArgs& a, const double* rec_dd, const TvlGaps& g, int TC) {
   constexpr int GPB = kDdBlock / L;
   const int grid = (a.B + GPB - 1) / GPB;
-  const size_t shmem = sizeof(double) * (size_t)(3 * a.N + 5 * TC + TC * a.N + GPB * kDPar + 2 * GPB * kTvlGaps) +
+  const size_t shmem = sizeof(double) * (size_t)(3 * a.N + 5 * TC + TC * a.N + GPB * kDPar + 2 * GPB * kDdWStride) +
                        sizeof(int) * a.N;
   if (shmem > 160 * 1024) return hipErrorInvalidValue;  // gfx950: 160 KiB of LDS per workgroup
   auto* k = a.rec_beta ? &tvl_dd_loglik_kernel<L, true> : &tvl_dd_loglik_kernel<L, false>;
