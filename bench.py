@@ -327,6 +327,9 @@ def main():
                     help="TVλ arithmetic (include/yfm.h yfm_set_precision; the library default is certified)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-rate", action="store_true",
+                    help="skip the host-pointer (PCIe-inclusive) timing, e.g. for PMC passes: its chunked "
+                         "dispatches would mix into the per-dispatch counter averages")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl = RCCL over xGMI (one GPU per rank); gloo = host collectives, ranks may share a GPU "
                          "(multi-rank rehearsal on a one-GPU box)")
@@ -451,7 +454,7 @@ def main():
     # host-pointer boundary (yfm_loglik_batch: θ in over PCIe, logliks back, synchronous) —
     # reported beside the metric, never as `value` (inputs are not HBM-resident there)
     host_rate = None
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1 and not args.no_host_rate:
         Th_host = np.asfortranarray(w.Theta)
         tu_host = w.T_use
         eng.loglik(kind, Th_host, space=0, T_use=tu_host)

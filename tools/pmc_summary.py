@@ -1,8 +1,15 @@
-"""Summarise rocprofv3 --pmc CSVs per kernel (average per dispatch) — used for profiles/*/pmc_summary.json."""
+"""Summarise rocprofv3 --pmc CSVs per kernel (average per dispatch) — used for profiles/*/pmc_summary.json.
+
+usage: pmc_summary.py [--evals B --steps S] <counter_collection.csv>...
+With --evals / --steps (the batch of one launch and its filter steps per eval, T − 1) the summary
+also carries the derived figures bench.py reads: executed FP64 flops per eval and per step
+((FMA·2 + ADD + MUL)·64 + MFMA_MOPS_F64·512, rocprof's SQ_INSTS_VALU_FLOPS_FP64 expression) and
+HBM bytes per launch (2·FETCH_SIZE + WRITE_SIZE, KiB → bytes: MI355X_MICROARCH.md's gfx950 correction).
+"""
+import argparse
 import collections
 import csv
 import json
-import sys
 from pathlib import Path
 
 
@@ -25,5 +32,29 @@ def summarise(paths, kernel_substr="loglik_kernel"):
     return out
 
 
+def derive(v, evals, steps):
+    if "SQ_INSTS_VALU_FMA_F64" in v:
+        f = (2 * v["SQ_INSTS_VALU_FMA_F64"] + v.get("SQ_INSTS_VALU_ADD_F64", 0) + v.get("SQ_INSTS_VALU_MUL_F64", 0)) * 64
+        f += v.get("SQ_INSTS_VALU_MFMA_MOPS_F64", 0) * 512
+        v["evals_per_launch"] = evals
+        v["fp64_flops_executed_per_eval"] = f / evals
+        v["fp64_flops_executed_per_step"] = f / evals / steps
+    if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
+        v["hbm_bytes_per_launch"] = (2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024
+    if "SQ_WAIT_ANY" in v and "SQ_WAVE_CYCLES" in v:
+        v["wait_any_frac"] = v["SQ_WAIT_ANY"] / v["SQ_WAVE_CYCLES"]
+    if "SQ_ACTIVE_INST_VALU" in v and "SQ_WAVE_CYCLES" in v:
+        v["valu_active_frac"] = v["SQ_ACTIVE_INST_VALU"] / v["SQ_WAVE_CYCLES"]
+
+
 if __name__ == "__main__":
-    print(json.dumps(summarise(sys.argv[1:]), indent=1))
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--evals", type=float, default=None)
+    ap.add_argument("--steps", type=float, default=None)
+    ap.add_argument("files", nargs="+")
+    a = ap.parse_args()
+    s = summarise(a.files)
+    if a.evals:
+        for v in s.values():
+            derive(v, a.evals, a.steps)
+    print(json.dumps(s, indent=1))

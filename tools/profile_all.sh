@@ -15,7 +15,7 @@ for c in 2 3 4 5; do
 done
 pass() { c=$1; name=$2; shift 2
   timeout -s KILL 120 rocprofv3 --pmc "$@" -d "$OUT/pmc_c${c}_$name" -o $name --output-format csv -- \
-    python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_c${c}_$name.log" 2>&1
+    python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-host-rate > "$OUT/pmc_c${c}_$name.log" 2>&1
   echo "pmc c$c $name ok"
 }
 for c in 2 3 5; do

@@ -5,7 +5,7 @@ set -e
 export TMPDIR=/tmp
 OUT=${1:-gpurun_out/prof}
 mkdir -p "$OUT"
-B="python bench.py --steps 3 --warmup 1 --no-cpu-baseline"
+B="python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-rate"
 pass() { name=$1; shift; timeout -s KILL 120 rocprofv3 --pmc "$@" -d "$OUT/pmc_$name" -o $name --output-format csv -- $B > "$OUT/pmc_$name.log" 2>&1; echo "pass $name rc=$?"; }
 pass valu SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES
 pass fetch FETCH_SIZE

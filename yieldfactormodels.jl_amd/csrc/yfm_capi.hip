@@ -246,6 +246,10 @@ int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int 
       YFM_HIP_CHECK(ctx->defer.ensure(sizeof(int) * (size_t)B));
       a.defer_count = reinterpret_cast<int*>(static_cast<unsigned int*>(ctx->flags.p) + 2);  // zeroed above
       a.defer_list = static_cast<int*>(ctx->defer.p);
+      if (const size_t sb = yfm::fixedz_scratch_bytes(kind, B)) {
+        YFM_HIP_CHECK(ctx->scratch.ensure(sb));
+        a.scratch = static_cast<double*>(ctx->scratch.p);
+      }
       e = yfm::launch_fixedz(kind, a);
       if (e == hipSuccess) e = yfm::launch_fixedz_group(kind, a);
     } else {

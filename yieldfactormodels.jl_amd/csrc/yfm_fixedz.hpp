@@ -97,7 +97,8 @@ struct FixedZFilter {
   double last_det = 0.0, last_q = 0.0;  // fresh model: F = 0, F⁻¹ = 0, v = 0 (kalmanbasemodel.jl:65-67)
 
   // G = Z'Z → R, log det G, collapsed vs capacitance; then initialize_filter.
-  __device__ __forceinline__ void setup(const double (&G)[M][M], int N_) {
+  // do_init = false: the caller loads the initial state itself (fixedz_init_kernel's record)
+  __device__ __forceinline__ void setup(const double (&G)[M][M], int N_, bool do_init = true) {
     N = N_;
     sigma2 = p.sigma2;
     rsig2 = 1.0 / sigma2;
@@ -140,7 +141,7 @@ struct FixedZFilter {
     for (int i = 0; i < M; ++i)
 #pragma unroll
       for (int j = 0; j < M; ++j) R[i][j] = collapsed ? sigma2 * 0.5 * (X[i][j] + X[j][i]) : G[i][j];
-    init_ok = init_state<M, LEAD>(p, beta, Pm);
+    if (do_init) init_ok = init_state<M, LEAD>(p, beta, Pm);
   }
 
   // One filter! call on column t given z̃_t (zc), (ȳ, ỹ'ỹ) = yb and (nan flag, y'y) = meta.

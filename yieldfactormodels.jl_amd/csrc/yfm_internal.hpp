@@ -18,7 +18,7 @@ struct LaunchArgs {
   unsigned int* flags;  // 2 device counters
   double* rec_beta;     // optional trajectories
   double* rec_P;
-  double* scratch;      // per-candidate work records (tvl_scratch_bytes)
+  double* scratch;      // per-candidate work records (tvl_scratch_bytes, fixedz_scratch_bytes)
   int horizon = 0;      // 0: loglik mode; ≥ 1: trajectory mode (predict / forecast / loss array)
   int rec_len = 0;      // recorded steps per candidate (the last rec_len), stride of rec_beta / rec_P
   int* defer_list = nullptr;   // per-lane fixed-loading kernel → lane-group kernel hand-off (B ints)
@@ -29,6 +29,8 @@ struct LaunchArgs {
 // padded maturity count NP the fixed-loading kernel is instantiated for (-1: none)
 int fixedz_np_for(int N);
 hipError_t launch_fixedz(int kind, const LaunchArgs& a);
+// per-candidate initial-state records of the per-lane kernel (GNS5: fixedz_init_kernel), bytes
+size_t fixedz_scratch_bytes(int kind, int B);
 // fixed-loading models with N beyond the per-lane kernel (yfm_group.hip): filter per lane group
 int group_max_n(int kind);
 int group_lanes_for(int kind, int N);

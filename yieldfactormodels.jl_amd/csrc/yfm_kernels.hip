@@ -33,6 +33,8 @@ namespace yfm {
 
 constexpr int kBlock = 256;  // 4 waves: one per SIMD of a CU
 constexpr int kTC = 32;      // panel columns per LDS chunk
+constexpr bool kMfma4 = true;   // GNS5 Z'ỹ on v_mfma_f64_4x4x4_4b_f64 (DNS keeps v_mfma_f64_16x16x4_f64)
+constexpr bool kZBasis = true;  // GNS5 fragments e = 1 − e^{−λm} against (ỹ, ỹ/m): see the kernel
 
 __global__ void prep_panel_kernel(const double* __restrict__ Y, int N, int T, int np, int ldp,
                                   double* __restrict__ out) {
@@ -60,6 +62,32 @@ __global__ void prep_panel_kernel(const double* __restrict__ Y, int N, int T, in
   o[np + 1] = tt;
   o[np + 2] = nan ? 1.0 : 0.0;
   o[np + 3] = yy;
+}
+
+// initialize_filter (filter.jl:1-10) for the 5-factor model in its own kernel: its 15×15
+// Lyapunov solve needs ~480 VGPRs, which inside the filter kernel forced the whole filter to spill
+// (≈2 KB per lane of scratch).  Writes β₀, the upper triangle of P₀ and the ok flag per candidate,
+// structure-of-arrays (rec[q·B + b]) so the filter kernel's reads are coalesced.
+template <int M>
+constexpr int fz_rec_len() { return M + M * (M + 1) / 2 + 1; }
+
+template <int M, int LEAD>
+__global__ __launch_bounds__(256) void fixedz_init_kernel(const double* __restrict__ theta, int P, int B, int space,
+                                                          double* __restrict__ rec) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  Params<M, LEAD> p;
+  decode_params<M, LEAD>(theta + (size_t)b * P, space, p);
+  double beta[M], Pm[M][M];
+  const bool ok = init_state<M, LEAD>(p, beta, Pm);
+  int q = 0;
+#pragma unroll
+  for (int i = 0; i < M; ++i) rec[(size_t)(q++) * B + b] = beta[i];
+#pragma unroll
+  for (int i = 0; i < M; ++i)
+#pragma unroll
+    for (int j = i; j < M; ++j) rec[(size_t)(q++) * B + b] = Pm[i][j];
+  rec[(size_t)q * B + b] = ok ? 1.0 : 0.0;
 }
 
 // ---- per-step building blocks (all __forceinline__: the fast path is one basic block) ----
@@ -107,8 +135,9 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     const double* __restrict__ theta, int P, int B, int space, const double* __restrict__ panel, int T, int N,
     const double* __restrict__ mats, const int* __restrict__ T_use, double* __restrict__ out,
     unsigned int* __restrict__ flags, double* __restrict__ rec_beta, double* __restrict__ rec_P, int horizon,
-    int rec_len, int* __restrict__ defer_list, int* __restrict__ defer_count) {
+    int rec_len, int* __restrict__ defer_list, int* __restrict__ defer_count, const double* __restrict__ init_rec) {
   constexpr int LDP = NP + 4;
+  constexpr bool SPLIT_INIT = (M == 5);  // initial state from fixedz_init_kernel
   constexpr int CH = kTC * LDP;               // doubles per chunk
   constexpr int PER = (CH + kBlock - 1) / kBlock;
   constexpr int NZ = M - 1;                   // non-constant loading columns
@@ -116,7 +145,15 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   constexpr int NK = (NP + 3) / 4;            // MFMA k-steps (4 maturities each)
   constexpr int NRT = 64 * NZ / 16;           // MFMA row tiles per wave (16 (cand, col) pairs each)
   constexpr int RGN = (NZ == 2) ? NRT : 4;    // row tiles accumulated at once (bounds live accumulators)
+  constexpr int RGN4 = (NZ == 2) ? NRT : 8;   // the same for the 4×4×4 form (one double per accumulator)
   constexpr int TB = 16;                      // steps per MFMA block
+  // GNS5 (two γ): the MFMA rows are e_l = 1 − e^{−λ_l m} (one per γ) against the panel columns ỹ and
+  // ỹ/m, so a candidate holds LEAD fragment rows instead of NZ = 2·LEAD:
+  //   Σ S_l ỹ = (1/λ_l) Σ e_l ỹ/m,   Σ C_l ỹ = Σ (S_l − z_l) ỹ = Σ S_l ỹ + Σ e_l ỹ   (Σ ỹ = 0),
+  // which halves the fragment registers (the 5-state filter no longer spills).
+  constexpr bool ZB = USE_MFMA && kMfma4 && kZBasis && LEAD == 2;
+  constexpr int RPC = ZB ? LEAD : NZ;         // fragment rows per candidate
+  constexpr int NRTA = 64 * RPC / 16;         // fragment row tiles per wave
   constexpr int SS = 64 * NZ + 2;             // scratch row stride (doubles): one row per step
   constexpr int SCR = USE_MFMA ? (TB * SS) : 2;
   static_assert(NZ == 2 * LEAD, "loading columns come in (S, C) pairs per gamma");
@@ -125,6 +162,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   __shared__ __attribute__((aligned(16))) double sh[2][CH];
   __shared__ __attribute__((aligned(16))) double scratch[kBlock / 64][SCR];
   __shared__ int s_nobs_max;
+  __shared__ double s_rm[ZB ? NP : 1];  // 1/m_i (0 past N)
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -135,6 +173,9 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   const int nobs = T_use ? T_use[bb] : T;
 
   if (tid == 0) s_nobs_max = 0;
+  if constexpr (ZB) {
+    for (int i = tid; i < NP; i += kBlock) s_rm[i] = (i < N) ? 1.0 / mats[i] : 0.0;
+  }
   __syncthreads();
   // loglik mode (horizon = 0): filter! over columns 0 .. nobs−2 (filter.jl:190).  Trajectory
   // mode (horizon ≥ 1, predict, filter.jl:250-282): columns 0 .. nobs−1, then horizon NaN
@@ -187,25 +228,37 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   // MFMA A fragments: tile r, k-step kk — lane l holds Z of pair p = 16r + (l & 15)
   // (candidate p >> 1 of this wave, column p & 1) at maturity 4kk + (l >> 4).
   // Gathered once through the wave's scratch, 16 candidates at a time.
-  double Af[USE_MFMA ? NRT : 1][USE_MFMA ? NK : 1];
+  double Af[USE_MFMA ? NRTA : 1][USE_MFMA ? NK : 1];
+  double rlam[LEAD];  // 1/λ_l (z-basis fragments)
+#pragma unroll
+  for (int l = 0; l < LEAD; ++l) rlam[l] = 1.0 / (1e-2 + exp(p.gam[l]));
   if constexpr (USE_MFMA) {
     constexpr int ZS = 4 * NK + 1;  // maturity stride of the staging image (odd: conflict-free LDS)
-    constexpr int QT = NRT / 4;  // row tiles per quarter (16 candidates)
-    static_assert(16 * NZ * ZS <= SCR, "staging fits the scratch");
+    constexpr int QT = NRTA / 4;  // row tiles per quarter (16 candidates)
+    static_assert(16 * RPC * ZS <= SCR, "staging fits the scratch");
     double* st = scratch[wave];
 #pragma unroll
     for (int qu = 0; qu < 4; ++qu) {
       if ((lane >> 4) == qu) {
         const int cl = lane & 15;
+        if constexpr (ZB) {
 #pragma unroll
-        for (int c = 0; c < NZ; ++c)
+          for (int l = 0; l < LEAD; ++l) {
+            const double lam = 1e-2 + exp(p.gam[l]);
 #pragma unroll
-          for (int m = 0; m < ZS; ++m) st[(cl * NZ + c) * ZS + m] = (m < NP) ? Zc[c][m] : 0.0;
+            for (int m = 0; m < ZS; ++m) st[(cl * RPC + l) * ZS + m] = (m < N) ? 1.0 - exp(-(lam * mats[m])) : 0.0;
+          }
+        } else {
+#pragma unroll
+          for (int c = 0; c < NZ; ++c)
+#pragma unroll
+            for (int m = 0; m < ZS; ++m) st[(cl * NZ + c) * ZS + m] = (m < NP) ? Zc[c][m] : 0.0;
+        }
       }
       __syncthreads();
 #pragma unroll
       for (int r = qu * QT; r < (qu + 1) * QT; ++r) {
-        const int pr = 16 * r + (lane & 15) - qu * 16 * NZ;  // pair index within this quarter
+        const int pr = 16 * r + (lane & 15) - qu * 16 * RPC;  // pair index within this quarter
 #pragma unroll
         for (int kk = 0; kk < NK; ++kk) Af[r][kk] = st[pr * ZS + 4 * kk + (lane >> 4)];
       }
@@ -215,7 +268,21 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
 
   FixedZFilter<M, LEAD, RECORD, false> f;
   f.p = p;
-  f.setup(G, N);
+  f.setup(G, N, !SPLIT_INIT);
+  if constexpr (SPLIT_INIT) {
+    int q = 0;
+#pragma unroll
+    for (int i = 0; i < M; ++i) f.beta[i] = init_rec[(size_t)(q++) * B + bb];
+#pragma unroll
+    for (int i = 0; i < M; ++i)
+#pragma unroll
+      for (int j = i; j < M; ++j) {
+        const double v = init_rec[(size_t)(q++) * B + bb];
+        f.Pm[i][j] = v;
+        f.Pm[j][i] = v;
+      }
+    f.init_ok = init_rec[(size_t)q * B + bb] != 0.0;
+  }
   // ill-conditioned Z'Z: this candidate is evaluated by the lane-group kernel instead (capacitance
   // form with the innovation formed per maturity); its lane here runs along without writing
   const bool defer = live && !f.collapsed;
@@ -285,28 +352,92 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     for (int t0 = 0; t0 < nsteps; t0 += TB) {
       // ---- z̃ for steps t0 .. t0+15 of all 64 candidates: NRT·NK MFMAs ----
       const double* cb = col_of(t0);  // TB consecutive columns of one chunk
-      double bvk[NK];
+      if constexpr (ZB) {
+        // rows: pair 16r + 4blk + i = (candidate, γ index); columns j of step pair sp: step
+        // 2sp + (j >> 1), ỹ (j even) or ỹ/m (j odd)
 #pragma unroll
-      for (int kk = 0; kk < NK; ++kk) {
-        const int m = 4 * kk + (lane >> 4);
-        bvk[kk] = (m < NP) ? cb[(lane & 15) * LDP + m] : 0.0;  // B[k = m][col = step]
-      }
+        for (int sp = 0; sp < TB / 2; ++sp) {
+          double bv[NK];
 #pragma unroll
-      for (int r0 = 0; r0 < NRT; r0 += RGN) {
-        yfm_double4 acc[RGN];
+          for (int kk = 0; kk < NK; ++kk) {
+            const int m = 4 * kk + (lane >> 4);
+            const double y = (m < NP) ? cb[(2 * sp + ((lane & 3) >> 1)) * LDP + m] : 0.0;
+            bv[kk] = (lane & 1) ? y * s_rm[m < NP ? m : 0] : y;
+          }
 #pragma unroll
-        for (int r = 0; r < RGN; ++r) acc[r] = yfm_double4{0.0, 0.0, 0.0, 0.0};
+          for (int r0 = 0; r0 < NRTA; r0 += NRTA) {
+            double acc[NRTA];
 #pragma unroll
-        for (int kk = 0; kk < NK; ++kk)
+            for (int r = 0; r < NRTA; ++r) acc[r] = 0.0;
+#pragma unroll
+            for (int kk = 0; kk < NK; ++kk)
+#pragma unroll
+              for (int r = 0; r < NRTA; ++r)
+                acc[r] = __builtin_amdgcn_mfma_f64_4x4x4f64(Af[r][kk], bv[kk], acc[r], 0, 0, 0);
+            // lane l: pair 16r + 4((l >> 2) & 3) + (l >> 4), step 2sp + ((l & 3) >> 1), column l & 1;
+            // per step a candidate's four values are (Σe₁ỹ, Σe₁ỹ/m, Σe₂ỹ, Σe₂ỹ/m)
+#pragma unroll
+            for (int r = 0; r < NRTA; ++r)
+              scr[(2 * sp + ((lane & 3) >> 1)) * SS + 2 * (16 * r + 4 * ((lane >> 2) & 3) + (lane >> 4)) + (lane & 1)] =
+                  acc[r];
+          }
+        }
+      } else if constexpr (kMfma4 && NZ == 4) {
+        // v_mfma_f64_4x4x4_4b_f64: block blk of instruction (r, s, kk) is D[4×4] = A[4 pairs ×
+        // 4 maturities]·B[4 maturities × 4 steps] for pairs 16r + 4blk + i, steps 4s + j,
+        // maturities 4kk + k.  Operand lanes (tools/mfma_f64_4x4_probe.hip): A[blk][i][k] in
+        // lane 16k + 4blk + i — exactly the 16×16×4 A fragment above — B[blk][k][j] in lane
+        // 16k + 4blk + j (the same panel values for every block), D[blk][i][j] in lane
+        // 16i + 4blk + j.  512 flops per instruction at ≈17 cycles vs 2,048 at ≈144 for the
+        // 16×16×4 form at one wave per SIMD (profiles/r2/micro).
+#pragma unroll
+        for (int s = 0; s < TB / 4; ++s) {
+          double bv[NK];
+#pragma unroll
+          for (int kk = 0; kk < NK; ++kk) {
+            const int m = 4 * kk + (lane >> 4);
+            bv[kk] = (m < NP) ? cb[(4 * s + (lane & 3)) * LDP + m] : 0.0;
+          }
+#pragma unroll
+          for (int r0 = 0; r0 < NRT; r0 += RGN4) {
+            double acc[RGN4];
+#pragma unroll
+            for (int r = 0; r < RGN4; ++r) acc[r] = 0.0;
+#pragma unroll
+            for (int kk = 0; kk < NK; ++kk)
+#pragma unroll
+              for (int r = 0; r < RGN4; ++r)
+                acc[r] = __builtin_amdgcn_mfma_f64_4x4x4f64(Af[r0 + r][kk], bv[kk], acc[r], 0, 0, 0);
+            // lane l holds pair 16r + 4((l >> 2) & 3) + (l >> 4) at step 4s + (l & 3)
+#pragma unroll
+            for (int r = 0; r < RGN4; ++r)
+              scr[(4 * s + (lane & 3)) * SS + 16 * (r0 + r) + 4 * ((lane >> 2) & 3) + (lane >> 4)] = acc[r];
+          }
+        }
+      } else {
+        double bvk[NK];
+#pragma unroll
+        for (int kk = 0; kk < NK; ++kk) {
+          const int m = 4 * kk + (lane >> 4);
+          bvk[kk] = (m < NP) ? cb[(lane & 15) * LDP + m] : 0.0;  // B[k = m][col = step]
+        }
+#pragma unroll
+        for (int r0 = 0; r0 < NRT; r0 += RGN) {
+          yfm_double4 acc[RGN];
+#pragma unroll
+          for (int r = 0; r < RGN; ++r) acc[r] = yfm_double4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int kk = 0; kk < NK; ++kk)
+#pragma unroll
+            for (int r = 0; r < RGN; ++r)
+              acc[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(Af[r0 + r][kk], bvk[kk], acc[r], 0, 0, 0);
+          // D[row = pair][col = step]: lane l holds step l & 15, pairs 16r + (l >> 4) + 4q
 #pragma unroll
           for (int r = 0; r < RGN; ++r)
-            acc[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(Af[r0 + r][kk], bvk[kk], acc[r], 0, 0, 0);
-        // D[row = pair][col = step]: lane l holds step l & 15, pairs 16r + (l >> 4) + 4q
 #pragma unroll
-        for (int r = 0; r < RGN; ++r)
-#pragma unroll
-          for (int q4 = 0; q4 < 4; ++q4)
-            scr[(lane & 15) * SS + 16 * (r0 + r) + (lane >> 4) + 4 * q4] = acc[r][q4];
+            for (int q4 = 0; q4 < 4; ++q4)
+              scr[(lane & 15) * SS + 16 * (r0 + r) + (lane >> 4) + 4 * q4] = acc[r][q4];
+        }
       }
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's scratch writes landed
       __builtin_amdgcn_wave_barrier();
@@ -317,8 +448,13 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
 #pragma unroll
         for (int j = 0; j < NZ; j += 2) {
           const double2 v = *reinterpret_cast<const double2*>(sp + j);
-          z[j] = v.x;
-          z[j + 1] = v.y;
+          if constexpr (ZB) {
+            z[j] = rlam[j / 2] * v.y;  // Σ S ỹ
+            z[j + 1] = z[j] + v.x;     // Σ C ỹ
+          } else {
+            z[j] = v.x;
+            z[j + 1] = v.y;
+          }
         }
       };
       double zc[NZ];
@@ -385,16 +521,25 @@ namespace yfm {
 template <int NP, int M, int LEAD>
 static hipError_t launch_fixedz_np(const LaunchArgs& a) {
   const int grid = (a.B + kBlock - 1) / kBlock;
+  if constexpr (M == 5) {
+    if (!a.scratch) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((fixedz_init_kernel<M, LEAD>), dim3(grid), dim3(kBlock), 0, a.stream, a.theta, a.P, a.B,
+                       a.space, a.scratch);
+  }
   if (a.rec_beta) {
     hipLaunchKernelGGL((fixedz_loglik_kernel<NP, M, LEAD, true>), dim3(grid), dim3(kBlock), 0, a.stream, a.theta, a.P,
                        a.B, a.space, a.panel, a.T, a.N, a.mats, a.T_use, a.out, a.flags, a.rec_beta, a.rec_P,
-                       a.horizon, a.rec_len, a.defer_list, a.defer_count);
+                       a.horizon, a.rec_len, a.defer_list, a.defer_count, a.scratch);
   } else {
     hipLaunchKernelGGL((fixedz_loglik_kernel<NP, M, LEAD, false>), dim3(grid), dim3(kBlock), 0, a.stream, a.theta,
                        a.P, a.B, a.space, a.panel, a.T, a.N, a.mats, a.T_use, a.out, a.flags, nullptr, nullptr, 0, 0,
-                       a.defer_list, a.defer_count);
+                       a.defer_list, a.defer_count, a.scratch);
   }
   return hipGetLastError();
+}
+
+size_t fixedz_scratch_bytes(int kind, int B) {
+  return kind == 2 ? sizeof(double) * (size_t)fz_rec_len<5>() * (size_t)(B > 0 ? B : 1) : 0;
 }
 
 int fixedz_np_for(int N) {
