@@ -69,6 +69,15 @@ struct DevBuf {
 
 }  // namespace
 
+// Per-launch device work buffers.  A context owns one; the estimation driver adds one per extra
+// concurrent stream (launches in flight on different streams must not share them).
+struct yfm::Workspace {
+  DevBuf flags;       // 4 × unsigned int: n_init_throw, n_neg_inf, deferred-candidate count, pad
+  DevBuf scratch;     // per-candidate work records (TVλ / GNS5 / two-wave DNS init)
+  DevBuf scratch_dd;  // TVλ double-double records (YFM_PREC_CERTIFIED)
+  DevBuf defer;       // list of candidates handed from the per-lane to the group kernel
+};
+
 struct yfm_ctx {
   int device = 0;
   int precision = YFM_PREC_CERTIFIED;  // TVλ arithmetic (yfm_set_precision)
@@ -184,11 +193,15 @@ struct PanelView {
 
 int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int B, const int* d_T_use,
            double* d_out, double* d_rb, double* d_rP, hipStream_t s, int horizon = 0, int rec_len = 0,
-           const PanelView* pv = nullptr, bool reset_flags = true) {
+           const PanelView* pv = nullptr, bool reset_flags = true, yfm::Workspace* ws = nullptr) {
+  DevBuf& w_flags = ws ? ws->flags : ctx->flags;
+  DevBuf& w_scratch = ws ? ws->scratch : ctx->scratch;
+  DevBuf& w_scratch_dd = ws ? ws->scratch_dd : ctx->scratch_dd;
+  DevBuf& w_defer = ws ? ws->defer : ctx->defer;
   // one fill resets the flag counters (unless a pipelined chunk continues them) and the
   // deferred-candidate count: flags.p = [n_init_throw, n_neg_inf, defer_count, pad]
   {
-    unsigned int* f = static_cast<unsigned int*>(ctx->flags.p);
+    unsigned int* f = static_cast<unsigned int*>(w_flags.p);
     YFM_HIP_CHECK(hipMemsetAsync(reset_flags ? f : f + 2, 0, (reset_flags ? 3 : 1) * sizeof(unsigned int), s));
   }
   if (B == 0) return YFM_OK;
@@ -206,7 +219,7 @@ int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int 
   a.mats = static_cast<const double*>(ctx->mats.p);
   a.T_use = d_T_use;
   a.out = d_out;
-  a.flags = static_cast<unsigned int*>(ctx->flags.p);
+  a.flags = static_cast<unsigned int*>(w_flags.p);
   a.rec_beta = d_rb;
   a.rec_P = d_rP;
   a.scratch = nullptr;
@@ -228,14 +241,14 @@ int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int 
     yfm::TvlGaps g;
     if (ctx->precision == YFM_PREC_CERTIFIED) {
       lanes = yfm::tvl_dd_lanes_for(B, ctx->N, std::getenv("YFM_TVL_LANES") ? lanes : 0);
-      YFM_HIP_CHECK(ctx->scratch_dd.ensure(yfm::tvl_dd_scratch_bytes(B, a.T)));
-      double* rdd = static_cast<double*>(ctx->scratch_dd.p);
+      YFM_HIP_CHECK(w_scratch_dd.ensure(yfm::tvl_dd_scratch_bytes(B, a.T)));
+      double* rdd = static_cast<double*>(w_scratch_dd.p);
       if (int r = tvl_gaps(ctx, lanes, g)) return r;
       e = yfm::launch_tvl_dd_init(a, rdd);
       if (e == hipSuccess) e = yfm::launch_tvl_dd(a, rdd, g, lanes);
     } else {
-      YFM_HIP_CHECK(ctx->scratch.ensure(yfm::tvl_scratch_bytes(B)));
-      a.scratch = static_cast<double*>(ctx->scratch.p);
+      YFM_HIP_CHECK(w_scratch.ensure(yfm::tvl_scratch_bytes(B)));
+      a.scratch = static_cast<double*>(w_scratch.p);
       if (int r = tvl_gaps(ctx, lanes, g)) return r;
       e = yfm::launch_tvl(a, g, lanes);
     }
@@ -243,12 +256,12 @@ int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int 
     // N ≤ 64: one filter per lane (MFMA Z'y), then the lane-group kernel for the candidates it
     // deferred (ill-conditioned Z'Z); larger N: one filter per lane group for every candidate
     if (yfm::fixedz_np_for(ctx->N) > 0) {
-      YFM_HIP_CHECK(ctx->defer.ensure(sizeof(int) * (size_t)B));
-      a.defer_count = reinterpret_cast<int*>(static_cast<unsigned int*>(ctx->flags.p) + 2);  // zeroed above
-      a.defer_list = static_cast<int*>(ctx->defer.p);
+      YFM_HIP_CHECK(w_defer.ensure(sizeof(int) * (size_t)B));
+      a.defer_count = reinterpret_cast<int*>(static_cast<unsigned int*>(w_flags.p) + 2);  // zeroed above
+      a.defer_list = static_cast<int*>(w_defer.p);
       if (const size_t sb = yfm::fixedz_scratch_bytes(kind, B)) {
-        YFM_HIP_CHECK(ctx->scratch.ensure(sb));
-        a.scratch = static_cast<double*>(ctx->scratch.p);
+        YFM_HIP_CHECK(w_scratch.ensure(sb));
+        a.scratch = static_cast<double*>(w_scratch.p);
       }
       e = yfm::launch_fixedz(kind, a);
       if (e == hipSuccess) e = yfm::launch_fixedz_group(kind, a);
@@ -501,6 +514,7 @@ int yfm_loglik_batch(yfm_ctx* ctx, int model_kind, int param_space, const double
   return YFM_OK;
 }
 
+
 int yfm_loglik_batch_device(yfm_ctx* ctx, int model_kind, int param_space, const double* d_theta, int P, int B,
                             const int* d_T_use, double* d_loglik_out, void* hip_stream) {
   if (int r = check_ctx(ctx)) return r;
@@ -664,3 +678,30 @@ int yfm_loss_array(yfm_ctx* ctx, int model_kind, int param_space, const double* 
 }
 
 }  // extern "C"
+
+namespace yfm {
+
+Workspace* workspace_create() {
+  auto* w = new Workspace;
+  if (w->flags.ensure(4 * sizeof(unsigned int)) != hipSuccess ||
+      hipMemset(w->flags.p, 0, 4 * sizeof(unsigned int)) != hipSuccess) {
+    delete w;
+    return nullptr;
+  }
+  return w;
+}
+
+void workspace_destroy(Workspace* w) {
+  if (!w) return;
+  for (DevBuf* b : {&w->flags, &w->scratch, &w->scratch_dd, &w->defer}) b->release();
+  delete w;
+}
+
+int loglik_device_ws(yfm_ctx* ctx, Workspace* ws, int kind, int space, const double* d_theta, int P, int B,
+                     const int* d_T_use, double* d_out, hipStream_t s) {
+  if (int r = check_ctx(ctx)) return r;
+  if (int r = check_batch(ctx, kind, space, P, B)) return r;
+  return launch(ctx, kind, space, d_theta, P, B, d_T_use, d_out, nullptr, nullptr, s, 0, 0, nullptr, true, ws);
+}
+
+}  // namespace yfm

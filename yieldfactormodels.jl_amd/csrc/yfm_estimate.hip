@@ -533,28 +533,52 @@ extern "C" int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const
     return yfm::api_error(YFM_EHIP, "hipHostMalloc failed for the estimation batch");
   double* th = static_cast<double*>(pin_th.p);
   double* out = static_cast<double*>(pin_out.p);
+  // Zero-copy rounds (default): the filter kernel reads θ from, and writes the logliks to, the
+  // page-locked buffers themselves — no DMA transfers to wait for between the host bookkeeping and
+  // the launch (θ is read once per lane, the loglik written once).
+  bool zero_copy = true;
+  if (const char* e = std::getenv("YFM_EST_ZEROCOPY")) zero_copy = std::atoi(e) != 0;
+  double *map_th = nullptr, *map_out = nullptr;
+  if (zero_copy && (hipHostGetDevicePointer(reinterpret_cast<void**>(&map_th), th, 0) != hipSuccess ||
+                    hipHostGetDevicePointer(reinterpret_cast<void**>(&map_out), out, 0) != hipSuccess))
+    zero_copy = false;
   std::memset(th, 0, sizeof(double) * (size_t)B * P);
   if (T_use)
     for (int r = 0; r < R; ++r) std::fill_n(static_cast<int*>(pin_tu.p) + (size_t)r * SLOT, SLOT, T_use[r]);
-  // device-side batch: θ uploaded per round on this call's own stream, T_use once
-  hipStream_t st = nullptr;
+  // Chains are split into G groups, each with its own stream and launch workspace: while one
+  // group's batch is on the device, the host consumes the other group's results and prepares its
+  // next round, and the two groups' filters run concurrently (each fills a small part of the chip),
+  // so a round costs one filter latency instead of filter + host bookkeeping + transfers.
+  int G = R >= 32 ? 2 : 1;
+  if (const char* e = std::getenv("YFM_EST_GROUPS")) G = std::max(1, std::min(2, std::atoi(e)));
+  // device-side batch: θ uploaded per round on each group's own stream, T_use once
+  hipStream_t sts[2] = {nullptr, nullptr};
+  yfm::Workspace* wss[2] = {nullptr, nullptr};  // group 0 uses the context's own buffers
   double *d_th = nullptr, *d_out = nullptr;
   int* d_tu = nullptr;
   struct Release {
-    hipStream_t& s;
+    hipStream_t (&s)[2];
+    yfm::Workspace* (&w)[2];
     double*& a;
     double*& b;
     int*& c;
     ~Release() {
-      if (s) (void)hipStreamSynchronize(s);
+      for (hipStream_t x : s)
+        if (x) (void)hipStreamSynchronize(x);
       if (a) (void)hipFree(a);
       if (b) (void)hipFree(b);
       if (c) (void)hipFree(c);
-      if (s) (void)hipStreamDestroy(s);
+      for (hipStream_t x : s)
+        if (x) (void)hipStreamDestroy(x);
+      for (yfm::Workspace* x : w) yfm::workspace_destroy(x);
     }
-  } release{st, d_th, d_out, d_tu};
-  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
-      hipMalloc(&d_th, sizeof(double) * (size_t)B * P) != hipSuccess ||
+  } release{sts, wss, d_th, d_out, d_tu};
+  for (int g = 0; g < G; ++g)
+    if (hipStreamCreateWithFlags(&sts[g], hipStreamNonBlocking) != hipSuccess)
+      return yfm::api_error(YFM_EHIP, "stream creation failed for the estimation batch");
+  if (G > 1 && !(wss[1] = yfm::workspace_create()))
+    return yfm::api_error(YFM_EHIP, "workspace allocation failed for the estimation batch");
+  if (hipMalloc(&d_th, sizeof(double) * (size_t)B * P) != hipSuccess ||
       hipMalloc(&d_out, sizeof(double) * (size_t)B) != hipSuccess ||
       (T_use && hipMalloc(&d_tu, sizeof(int) * (size_t)B) != hipSuccess))
     return yfm::api_error(YFM_EHIP, "device allocation failed for the estimation batch");
@@ -562,7 +586,7 @@ extern "C" int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const
     return yfm::api_error(YFM_EHIP, "T_use upload failed");
   int nthreads = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
   if (const char* e = std::getenv("YFM_EST_THREADS")) nthreads = std::max(1, std::atoi(e));
-  Pool pool(std::min(nthreads, std::max(1, R / 16)));
+  Pool pool(std::min(nthreads, std::max(1, R / (16 * G))));
   std::atomic<int> active{0};
   long long device_evals = 0, rounds = 0;
   double t_host = 0.0, t_dev = 0.0;
@@ -599,25 +623,60 @@ extern "C" int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const
     if (!c.spec.empty())
       std::memcpy(slot + c.trial.size(), c.spec_pts.data(), sizeof(double) * c.spec.size() * 4 * (size_t)P);
   };
-  for (;;) {
-    const auto t0 = clk::now();
+  // group g: chains [r0[g], r0[g + 1]), slots [r0[g]·SLOT, r0[g + 1]·SLOT) of every buffer
+  int r0[3] = {0, G > 1 ? R / 2 : R, R};
+  bool pending[2] = {false, false};
+  auto host_group = [&](int g) {
     active.store(0);
-    pool.run(R, 8, host_step);
-    if (active.load() == 0) break;
-    const auto t1 = clk::now();
-    if (hipMemcpyAsync(d_th, th, sizeof(double) * (size_t)B * P, hipMemcpyHostToDevice, st) != hipSuccess)
+    pool.run(r0[g + 1] - r0[g], 8, [&](int i) { host_step(r0[g] + i); });
+    return active.load() > 0;
+  };
+  auto submit = [&](int g) -> int {
+    const size_t o = (size_t)r0[g] * SLOT;
+    const int Bg = (r0[g + 1] - r0[g]) * SLOT;
+    if (zero_copy) {
+      const int rc = yfm::loglik_device_ws(ctx, wss[g], model_kind, YFM_THETA_UNCONSTRAINED, map_th + o * P, P, Bg,
+                                           d_tu ? d_tu + o : nullptr, map_out + o, sts[g]);
+      if (rc != YFM_OK) return rc;
+      device_evals += Bg;
+      ++rounds;
+      return YFM_OK;
+    }
+    if (hipMemcpyAsync(d_th + o * P, th + o * P, sizeof(double) * (size_t)Bg * P, hipMemcpyHostToDevice, sts[g]) !=
+        hipSuccess)
       return yfm::api_error(YFM_EHIP, "θ upload failed");
-    const int rc = yfm_loglik_batch_device(ctx, model_kind, YFM_THETA_UNCONSTRAINED, d_th, P, B, d_tu, d_out, st);
+    const int rc = yfm::loglik_device_ws(ctx, wss[g], model_kind, YFM_THETA_UNCONSTRAINED, d_th + o * P, P, Bg,
+                                         d_tu ? d_tu + o : nullptr, d_out + o, sts[g]);
     if (rc != YFM_OK) return rc;
-    if (hipMemcpyAsync(out, d_out, sizeof(double) * (size_t)B, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
+    if (hipMemcpyAsync(out + o, d_out + o, sizeof(double) * (size_t)Bg, hipMemcpyDeviceToHost, sts[g]) != hipSuccess)
       return yfm::api_error(YFM_EHIP, "loglik download failed");
-    const auto t2 = clk::now();
-    device_evals += B;
+    device_evals += Bg;
     ++rounds;
-    t_host += std::chrono::duration<double>(t1 - t0).count();
-    t_dev += std::chrono::duration<double>(t2 - t1).count();
+    return YFM_OK;
+  };
+  for (int g = 0; g < G; ++g) {
+    const auto t0 = clk::now();
+    pending[g] = host_group(g);
+    t_host += std::chrono::duration<double>(clk::now() - t0).count();
+    if (pending[g])
+      if (int rc = submit(g)) return rc;
   }
+  for (bool any = true; any;) {
+    any = false;
+    for (int g = 0; g < G; ++g) {
+      if (!pending[g]) continue;
+      const auto t0 = clk::now();
+      if (hipStreamSynchronize(sts[g]) != hipSuccess) return yfm::api_error(YFM_EHIP, "estimation round failed");
+      const auto t1 = clk::now();
+      pending[g] = host_group(g);
+      t_dev += std::chrono::duration<double>(t1 - t0).count();
+      t_host += std::chrono::duration<double>(clk::now() - t1).count();
+      if (pending[g])
+        if (int rc = submit(g)) return rc;
+      any = any || pending[g];
+    }
+  }
+  rounds = (rounds + G - 1) / G;  // rounds per group (each group's chains see one launch per round)
   long long evals = 0;
   long long hits = 0;
   for (const Chain& c : chains) {
@@ -626,8 +685,8 @@ extern "C" int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const
   }
   if (stats)
     std::fprintf(stderr, "yfm_estimate: %lld rounds, %lld chain evaluations, %lld device evaluations, %lld "
-                 "speculated iterations used; host %.3f s, loglik calls %.3f s\n", rounds, evals, device_evals,
-                 hits, t_host, t_dev);
+                 "speculated iterations used; host %.3f s, waiting on the device %.3f s (%d groups)\n", rounds, evals,
+                 device_evals, hits, t_host, t_dev, G);
   for (int r = 0; r < R; ++r) {
     const Chain& c = chains[r];
     const bool ok = c.status != 1;

@@ -83,6 +83,13 @@ hipError_t launch_init_bad(const double* ll, int B, unsigned char* bad, hipStrea
 hipError_t launch_predict_emit(const PredictArgs& a);
 hipError_t launch_forecast_emit(const PredictArgs& a);
 hipError_t launch_loss_array(const PredictArgs& a, const double* Y, int T1, int passes, unsigned int* flags);
+// Extra per-launch work buffers (flags, deferral list, init records) so launches can be in flight
+// on several streams of one context at once (yfm_capi.hip; used by the estimation driver).
+struct Workspace;
+Workspace* workspace_create();
+void workspace_destroy(Workspace* w);
+int loglik_device_ws(yfm_ctx* ctx, Workspace* ws, int kind, int space, const double* d_theta, int P, int B,
+                     const int* d_T_use, double* d_out, hipStream_t s);
 // record `msg` as yfm_last_error() for this thread and return `code` (host helpers above the C ABI)
 int api_error(int code, const char* msg);
 // columns of the context's panel (0 before yfm_set_panel)
