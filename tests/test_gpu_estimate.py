@@ -152,21 +152,25 @@ def test_estimate_init_is_the_rescaled_start(engine, panel):
 
 
 def test_speculation_is_bitwise_neutral(engine, panel):
-    """YFM_NM_SPEC=2 (two iterations per round, the default) vs 1 (one): the same chains bit for
-    bit and the same count of consumed evaluations, on 12 windows with rescaled and failing starts."""
+    """Speculation-tree budgets YFM_NM_SPEC = 1 (one iteration per round), 7, 16 (the default) and 32
+    nodes: the same chains bit for bit and the same count of consumed evaluations, on 12 windows
+    with rescaled and failing starts."""
     import os
     Y, mats = panel
     engine.set_panel(Y, mats)
     starts = S.theta_batch(KIND_DNS, 12, seed=67, bad_frac=0.2, scale=0.08)
     win = np.array([80, 79, 70, 66, 60, 55, 50, 45, 40, 33, 80, 72], dtype=np.int32)
     res = {}
-    for mode in ("1", "2"):
+    modes = ("1", "7", "16", "32")
+    for mode in modes:
         os.environ["YFM_NM_SPEC"] = mode
         try:
             res[mode] = engine.estimate(KIND_DNS, starts, space=0, T_use=win, iterations=200, max_group_iters=3)
         finally:
             os.environ.pop("YFM_NM_SPEC", None)
-    a, b = res["1"], res["2"]
-    for k in ("theta_c", "p", "init_c", "ll", "status"):
-        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
-    assert a["n_evals"] == b["n_evals"]
+    a = res["1"]
+    for mode in modes[1:]:
+        b = res[mode]
+        for k in ("theta_c", "p", "init_c", "ll", "status"):
+            np.testing.assert_array_equal(a[k], b[k], err_msg=f"{k} at {mode} nodes")
+        assert a["n_evals"] == b["n_evals"]

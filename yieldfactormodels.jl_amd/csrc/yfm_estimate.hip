@@ -24,15 +24,17 @@
 // costs one extra round.  The arithmetic of the simplex updates follows Optim's
 // operation order with FP contraction off, so the chain is bitwise reproducible.
 //
-// Two-iteration speculation (YFM_NM_SPEC=2, the default): the round that evaluates an
-// iteration's four trial points also evaluates the next iteration's four for each way this
-// one can end without a shrink â€” the accepted point (reflection, expansion, outside or
-// inside contraction) and whether it becomes the new worst vertex (only a contraction can):
-// six simplices, 24 more points.  After the real outcome is known, the chain's next trial
-// points are those of exactly one speculated simplex (same vertices, same worst index, so
-// the same arithmetic); its values are consumed at once and the iteration costs no round.
-// The chain's sequence of states, and so its result, is bitwise that of one iteration per
-// round; n_evals counts the evaluations the chain consumed (as without speculation).
+// Speculation tree (YFM_NM_SPEC = node budget per chain and round, default 16; 1 = none):
+// besides its iteration's four trial points, a round evaluates the trial points of later
+// iterations for the ways the earlier ones can end without a shrink â€” which trial point is
+// accepted and which vertex is then the worst (see build_tree).  Nodes are picked best-first by
+// the probability that the chain reaches them, estimated from the chain's own history of outcome
+// transitions.  When the real outcome of an iteration is known, the chain's next iteration is
+// the speculated node with the same simplex (same vertices, same worst index, so the same
+// arithmetic): its values are consumed at once and it costs no round; the walk continues down
+// the tree until an outcome was not speculated.  The chain's sequence of states, and so its
+// result, is bitwise that of one iteration per round; n_evals counts the evaluations the chain
+// consumed (as without speculation).
 #pragma clang fp contract(off)
 
 #include <hip/hip_runtime.h>
@@ -129,18 +131,38 @@ struct Chain {
   bool converged = false;
   std::vector<double> xc, xl, trial;  // centroid, best vertex, requested points
   int n_req = 0;
-  // speculation: the next iteration's trial points for each non-shrink outcome of this one
-  struct Spec {
-    int src;  // accepted trial point: 0 reflection, 1 expansion, 2 outside, 3 inside contraction
-    int hp;   // the worst vertex after the update
+  // speculation tree of this round (node 0 = the real iteration, see the file header)
+  struct Node {
+    int parent;  // -1 for node 0
+    int src;     // the parent's accepted trial point: 0 reflection, 1 expansion, 2 outside, 3 inside
+    int h;       // the worst vertex of this node's simplex
+    int kind;    // outcome kind of the parent's iteration this node assumes (outcome_kind)
+    int depth;   // iterations after the real one
+    double prob; // estimated probability that the chain reaches this node
   };
-  std::vector<Spec> spec;
-  std::vector<double> spec_pts;  // 4n per entry of spec, in request order after the 4 real points
-  std::vector<double> tmp;       // scratch of the speculation (centroid, saved vertex)
-  int acc_src = -1;              // accepted trial point of the last NM_ITER consume (-1: shrink)
-  long long used = 0;            // evaluations consumed by the chain
+  std::vector<Node> nodes;
+  std::vector<const double*> vx;  // nodes Ã— (n+1) vertex pointers (into S or an ancestor's points)
+  std::vector<double> pts;        // nodes Ã— 4n trial points (node 0's are also in trial)
+  std::vector<double> xcs;        // centroid scratch
+  std::vector<double> pre;        // (n+2) Ã— n storage-order prefix sums of the simplex
+  int acc_src = -1;               // accepted trial point of the last NM_ITER consume (-1: shrink)
+  long long used = 0;             // evaluations consumed by the chain
   long long spec_hits = 0;
+  long long depth_hist[8] = {};   // iterations consumed per round (stats)
+  // outcome kind of each iteration (outcome_kind), previous â†’ next; drives the tree's priorities
+  int last_kind = 7;
+  long long trans[8][8] = {};
+  int last_h = -1;              // the vertex the previous iteration replaced
+  long long recent[2] = {};     // "not the new vertex" outcomes: worst = last_h, all
 };
+
+// 0 reflection, 1 expansion, 2/3 outside contraction (3: the new vertex is the worst),
+// 4/5 inside contraction (5: the new vertex is the worst), 6 shrink
+int outcome_kind(const Chain& c, int ih) {
+  if (c.acc_src < 0) return 6;
+  const bool nw = c.order[c.n] == ih;
+  return c.acc_src <= 1 ? c.acc_src : 2 * c.acc_src - 2 + (nw ? 1 : 0);
+}
 
 void sortperm(Chain& c) {
   std::iota(c.order.begin(), c.order.end(), 0);
@@ -188,11 +210,21 @@ Params nm_parameters(int n) {  // Optim.AdaptiveParameters: (Î±, Î² + 2/n, Î³ âˆ
 
 // Nelderâ€“Mead trial points of the iteration whose worst vertex is h: centroid of the other
 // vertices (storage order), then reflection, expansion, outside and inside contraction
-void iter_trials(const Chain& c, int h, double* xc, double* trial) {
-  const int n = c.n;
+// of the simplex whose vertex v is vx[v] (centroid! with the same operation order as centroid).
+// pre = the storage-order partial sum of vertices 0..dâˆ’1 (0.0 + x_0 + â€¦ + x_{dâˆ’1}, as centroid
+// forms it), valid when none of them is h or differs from the simplex pre was summed over.
+void iter_trials(int n, const double* const* vx, int h, double* xc, double* trial, const double* pre, int d) {
   const Params q = nm_parameters(n);
-  centroid(c, h, xc);
-  const double* xh = &c.S[(size_t)h * n];
+  double acc[kMaxSlot];  // a local accumulator: no aliasing with the vertices, so it vectorises
+  for (int k = 0; k < n; ++k) acc[k] = pre[k];
+  for (int v = d; v <= n; ++v) {
+    if (v == h) continue;
+    const double* __restrict x = vx[v];
+    for (int k = 0; k < n; ++k) acc[k] = acc[k] + x[k];
+  }
+  const double r = 1.0 / n;
+  for (int k = 0; k < n; ++k) xc[k] = acc[k] * r;
+  const double* xh = vx[h];
   double* xr = trial;
   for (int k = 0; k < n; ++k) xr[k] = xc[k] + q.al * (xc[k] - xh[k]);
   for (int k = 0; k < n; ++k) {
@@ -203,11 +235,112 @@ void iter_trials(const Chain& c, int h, double* xc, double* trial) {
   }
 }
 
+// Speculation tree of an NM_ITER round (see the file header).  Node 0 is the real iteration on
+// the chain's simplex.  A child of node X assumes one way X's iteration ends without a shrink:
+// the accepted trial point src replaces X's worst vertex h_X, and hp is the worst vertex of the
+// result â€” h_X itself (only after a contraction), the worst vertex whose value is already known,
+// or one replaced earlier on the path (its value is not known yet).  Nodes are chosen best-first
+// by the estimated probability that the chain reaches them (products of the chain's own
+// outcome-transition frequencies), which maximises the expected iterations per round for the
+// node budget.  Every node's trial points are computed exactly as the real iteration would
+// compute them from that simplex (iter_trials on the same vertex coordinates, same worst index).
+constexpr int kMaxNodes = 32;
+constexpr int kMaxGroups = 4;
+
+void build_tree(Chain& c, int budget, int max_depth) {
+  const int n = c.n, m = n + 1;
+  const size_t w = (size_t)4 * n;
+  budget = std::max(1, std::min(budget, kMaxNodes));
+  c.nodes.clear();
+  c.nodes.reserve(budget);
+  c.vx.resize((size_t)budget * m);
+  c.pts.resize((size_t)budget * w);  // sized once: children point into it
+  c.xcs.resize(n);
+  // pre[v] = 0.0 + x_0 + â€¦ + x_{vâˆ’1} over the chain's simplex: every node's centroid sum starts
+  // from the longest prefix of vertices it shares with it
+  c.pre.resize((size_t)(m + 1) * n);
+  for (int k = 0; k < n; ++k) c.pre[k] = 0.0;
+  for (int v = 0; v < m; ++v)
+    for (int k = 0; k < n; ++k) c.pre[(size_t)(v + 1) * n + k] = c.pre[(size_t)v * n + k] + c.S[(size_t)v * n + k];
+  auto trials = [&](const double* const* v, int h, double* out) {
+    int d = 0;
+    while (d < h && v[d] == &c.S[(size_t)d * n]) ++d;
+    iter_trials(n, v, h, c.xcs.data(), out, &c.pre[(size_t)d * n], d);
+  };
+  c.nodes.push_back({-1, -1, c.order[n], c.last_kind, 0, 1.0});
+  for (int v = 0; v < m; ++v) c.vx[v] = &c.S[(size_t)v * n];
+  trials(c.vx.data(), c.order[n], c.pts.data());
+  if (budget == 1 || max_depth <= 0) return;
+  // P(next kind | previous kind) from the chain's counts plus one pseudo-count per kind;
+  // rq: share of "not the new vertex" outcomes whose worst is the previously replaced vertex
+  double pk[8][7];
+  for (int a = 0; a < 8; ++a) {
+    double s = 0.0;
+    for (int b = 0; b < 7; ++b) s += (double)c.trans[a][b] + 1.0;
+    for (int b = 0; b < 7; ++b) pk[a][b] = ((double)c.trans[a][b] + 1.0) / s;
+  }
+  const double rq = ((double)c.recent[0] + 1.0) / ((double)c.recent[1] + 2.0);
+  struct Cand {
+    int parent, src, h, kind;
+    double prob;
+  };
+  Cand cand[kMaxNodes * 4 * 8];  // a max-heap on prob
+  int nc = 0;
+  auto by_prob = [](const Cand& a, const Cand& b) { return a.prob < b.prob; };
+  unsigned char mark[kMaxSlot];
+  auto expand = [&](int x) {
+    const Chain::Node X = c.nodes[x];
+    if (X.depth >= max_depth) return;
+    std::memset(mark, 0, (size_t)m);
+    int nu = 0;  // vertices replaced on the path to X, other than h_X
+    for (int p = x; c.nodes[p].parent >= 0; p = c.nodes[p].parent) {
+      const int u = c.nodes[c.nodes[p].parent].h;
+      if (u != X.h && !mark[u]) ++nu;
+      mark[u] = 1;
+    }
+    mark[X.h] = 1;
+    int wk = -1;  // the worst vertex with a known value
+    for (int i = n; i >= 0; --i)
+      if (!mark[c.order[i]]) {
+        wk = c.order[i];
+        break;
+      }
+    const double* row = pk[X.kind];
+    auto push = [&](int src, int h, int kind, double p) {
+      if (p < 1e-4 || nc >= (int)(sizeof(cand) / sizeof(cand[0]))) return;
+      cand[nc++] = {x, src, h, kind, p};
+      std::push_heap(cand, cand + nc, by_prob);
+    };
+    for (int src = 0; src < 4; ++src) {
+      const int kn = src <= 1 ? src : 2 * src - 2;  // the new vertex is not the worst
+      if (src >= 2) push(src, X.h, kn + 1, X.prob * row[kn + 1]);
+      const double pn = X.prob * row[kn];
+      if (wk >= 0) push(src, wk, kn, pn * (nu ? 1.0 - rq : 1.0));
+      if (nu)
+        for (int u = 0; u < m; ++u)
+          if (mark[u] && u != X.h) push(src, u, kn, pn * rq / nu);
+    }
+  };
+  expand(0);
+  while ((int)c.nodes.size() < budget && nc > 0) {
+    std::pop_heap(cand, cand + nc, by_prob);
+    const Cand k = cand[--nc];
+    const int id = (int)c.nodes.size();
+    const Chain::Node P = c.nodes[k.parent];
+    c.nodes.push_back({k.parent, k.src, k.h, k.kind, P.depth + 1, k.prob});
+    const double** v = &c.vx[(size_t)id * m];
+    std::copy(&c.vx[(size_t)k.parent * m], &c.vx[(size_t)(k.parent + 1) * m], v);
+    v[P.h] = &c.pts[(size_t)k.parent * w + (size_t)k.src * n];
+    trials(v, k.h, &c.pts[(size_t)id * w]);
+    expand(id);
+  }
+}
+
 // Queue the points chain c needs this round; advances phases that need no evaluation.
-void prepare(Chain& c, int iterations, int spec_depth) {
+void prepare(Chain& c, int iterations, int spec_nodes) {
   const int n = c.n, m = n + 1;
   c.n_req = 0;
-  c.spec.clear();
+  c.nodes.clear();
   if (c.phase == NM_ITER && (c.converged || c.it >= iterations)) c.phase = NM_FINAL;
   c.trial.clear();
   switch (c.phase) {
@@ -225,33 +358,14 @@ void prepare(Chain& c, int iterations, int spec_depth) {
       c.order.assign(m, 0);
       c.it = 0;
       c.converged = false;
+      c.last_kind = 7;
       c.trial = c.S;
       break;
     }
-    case NM_ITER: {
-      c.xc.assign(n, 0.0);
-      c.trial.assign((size_t)4 * n, 0.0);
-      iter_trials(c, c.order[m - 1], c.xc.data(), c.trial.data());
-      if (spec_depth >= 2) {
-        // the six simplices the next iteration can start from (see the file header)
-        static const Chain::Spec kinds[6] = {{0, 0}, {1, 0}, {2, 0}, {2, 1}, {3, 0}, {3, 1}};
-        const int ih = c.order[m - 1], ish = c.order[m - 2];
-        c.spec_pts.resize((size_t)6 * 4 * n);
-        c.tmp.resize((size_t)2 * n);
-        double* xc2 = c.tmp.data();
-        double* saved = xc2 + n;
-        double* vh = &c.S[(size_t)ih * n];
-        std::copy(vh, vh + n, saved);
-        for (int k = 0; k < 6; ++k) {
-          const int src = kinds[k].src, hp = kinds[k].hp ? ih : ish;
-          c.spec.push_back({src, hp});
-          std::copy(&c.trial[(size_t)src * n], &c.trial[(size_t)(src + 1) * n], vh);
-          iter_trials(c, hp, xc2, &c.spec_pts[(size_t)k * 4 * n]);
-        }
-        std::copy(saved, saved + n, vh);
-      }
+    case NM_ITER:
+      build_tree(c, spec_nodes, iterations - c.it - 1);
+      c.trial.assign(c.pts.begin(), c.pts.begin() + (size_t)4 * n);
       break;
-    }
     case NM_SHRINK: {
       const Params q = nm_parameters(n);
       c.trial.assign((size_t)n * n, 0.0);
@@ -516,14 +630,14 @@ extern "C" int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const
       c.p[i] = std::isfinite(x) ? x : 0.0;  // _sanitize_parameters (optimization.jl:422-432)
     }
   }
-  int spec_depth = 2;
-  if (const char* e = std::getenv("YFM_NM_SPEC")) spec_depth = std::atoi(e);
+  int spec_nodes = 16;
+  if (const char* e = std::getenv("YFM_NM_SPEC")) spec_nodes = std::max(1, std::min(kMaxNodes, std::atoi(e)));
   const bool stats = std::getenv("YFM_EST_STATS") != nullptr;
   // Every chain owns a fixed slot of SLOT points in the round's batch (its requests, then its
   // speculated points; the rest of the slot keeps earlier values and its results are ignored),
   // so each chain's host work â€” consume the last results, prepare, write the slot â€” runs in
   // parallel, straight into page-locked memory, and T_use is written once.
-  const int SLOT = std::max(spec_depth >= 2 ? 28 : 4, P + 1);
+  const int SLOT = std::max(4 * spec_nodes, P + 1);
   if (SLOT > kMaxSlot) return yfm::api_error(YFM_EINVAL, "too many parameters for the estimation driver");
   const int B = R * SLOT;
   PinnedBuf pin_th, pin_tu, pin_out;
@@ -550,15 +664,15 @@ extern "C" int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const
   // next round, and the two groups' filters run concurrently (each fills a small part of the chip),
   // so a round costs one filter latency instead of filter + host bookkeeping + transfers.
   int G = R >= 32 ? 2 : 1;
-  if (const char* e = std::getenv("YFM_EST_GROUPS")) G = std::max(1, std::min(2, std::atoi(e)));
+  if (const char* e = std::getenv("YFM_EST_GROUPS")) G = std::max(1, std::min(kMaxGroups, std::atoi(e)));
   // device-side batch: Î¸ uploaded per round on each group's own stream, T_use once
-  hipStream_t sts[2] = {nullptr, nullptr};
-  yfm::Workspace* wss[2] = {nullptr, nullptr};  // group 0 uses the context's own buffers
+  hipStream_t sts[kMaxGroups] = {};
+  yfm::Workspace* wss[kMaxGroups] = {};  // group 0 uses the context's own buffers
   double *d_th = nullptr, *d_out = nullptr;
   int* d_tu = nullptr;
   struct Release {
-    hipStream_t (&s)[2];
-    yfm::Workspace* (&w)[2];
+    hipStream_t (&s)[kMaxGroups];
+    yfm::Workspace* (&w)[kMaxGroups];
     double*& a;
     double*& b;
     int*& c;
@@ -576,8 +690,9 @@ extern "C" int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const
   for (int g = 0; g < G; ++g)
     if (hipStreamCreateWithFlags(&sts[g], hipStreamNonBlocking) != hipSuccess)
       return yfm::api_error(YFM_EHIP, "stream creation failed for the estimation batch");
-  if (G > 1 && !(wss[1] = yfm::workspace_create()))
-    return yfm::api_error(YFM_EHIP, "workspace allocation failed for the estimation batch");
+  for (int g = 1; g < G; ++g)
+    if (!(wss[g] = yfm::workspace_create()))
+      return yfm::api_error(YFM_EHIP, "workspace allocation failed for the estimation batch");
   if (hipMalloc(&d_th, sizeof(double) * (size_t)B * P) != hipSuccess ||
       hipMalloc(&d_out, sizeof(double) * (size_t)B) != hipSuccess ||
       (T_use && hipMalloc(&d_tu, sizeof(int) * (size_t)B) != hipSuccess))
@@ -586,7 +701,7 @@ extern "C" int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const
     return yfm::api_error(YFM_EHIP, "T_use upload failed");
   int nthreads = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
   if (const char* e = std::getenv("YFM_EST_THREADS")) nthreads = std::max(1, std::atoi(e));
-  Pool pool(std::min(nthreads, std::max(1, R / (16 * G))));
+  Pool pool(std::min(nthreads, std::max(1, R / (4 * G))));
   std::atomic<int> active{0};
   long long device_evals = 0, rounds = 0;
   double t_host = 0.0, t_dev = 0.0;
@@ -595,40 +710,66 @@ extern "C" int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const
     Chain& c = chains[r];
     if (c.n_req > 0) {  // the results of this chain's slot from the last round
       double f[kMaxSlot];
-      const int nv = c.n_req + 4 * (int)c.spec.size();
+      const int nv = c.nodes.empty() ? c.n_req : 4 * (int)c.nodes.size();
       for (int k = 0; k < nv; ++k) f[k] = -out[(size_t)r * SLOT + k];  // compute_loss = âˆ’loglik (optimization.jl:22)
+      // outcome statistics of every NM iteration: they set the speculation tree's priorities
+      auto note = [&](int ih) {
+        if (c.phase == DONE) return;
+        const int k = outcome_kind(c, ih);
+        ++c.trans[c.last_kind][k];
+        c.last_kind = k;
+        if (k == 0 || k == 1 || k == 2 || k == 4) {
+          ++c.recent[1];
+          if (c.order[c.n] == c.last_h && c.last_h != ih) ++c.recent[0];
+        }
+        c.last_h = ih;
+      };
+      const Phase ph0 = c.phase;
+      const int ih0 = ph0 == NM_ITER ? c.order[c.n] : -1;
       consume(c, f, max_group_iters, tol, g_tol);
       c.used += c.n_req;
-      // a speculated next iteration whose simplex is the one the chain now holds
-      if (c.phase == NM_ITER && c.acc_src >= 0 && !c.converged && c.it < iterations) {
-        const int hp = c.order[c.n];
-        for (size_t k = 0; k < c.spec.size(); ++k) {
-          if (c.spec[k].src != c.acc_src || c.spec[k].hp != hp) continue;
-          const size_t w = (size_t)4 * c.n;
-          c.trial.assign(c.spec_pts.begin() + k * w, c.spec_pts.begin() + (k + 1) * w);
-          c.spec.clear();
-          consume(c, f + 4 + 4 * k, max_group_iters, tol, g_tol);
+      if (ph0 == NM_ITER) {
+        note(ih0);
+        // walk down the speculation tree while the chain's real state is a speculated node's
+        int cur = 0, done = 1;
+        const size_t w = (size_t)4 * c.n;
+        while (c.phase == NM_ITER && c.acc_src >= 0 && !c.converged && c.it < iterations) {
+          const int hp = c.order[c.n];
+          int nxt = -1;
+          for (int k = 1; k < (int)c.nodes.size(); ++k)
+            if (c.nodes[k].parent == cur && c.nodes[k].src == c.acc_src && c.nodes[k].h == hp) {
+              nxt = k;
+              break;
+            }
+          if (nxt < 0) break;
+          c.trial.assign(c.pts.begin() + nxt * w, c.pts.begin() + (nxt + 1) * w);
+          consume(c, f + 4 * nxt, max_group_iters, tol, g_tol);
+          note(hp);
           c.used += 4;
           ++c.spec_hits;
-          break;
+          cur = nxt;
+          ++done;
         }
+        ++c.depth_hist[std::min(done, 7)];
       }
-      c.spec.clear();
+      c.nodes.clear();
     }
-    prepare(c, iterations, spec_depth);
+    prepare(c, iterations, spec_nodes);
     if (c.n_req == 0) return;
     active.fetch_add(1, std::memory_order_relaxed);
     double* slot = th + (size_t)r * SLOT * P;
-    std::memcpy(slot, c.trial.data(), sizeof(double) * c.trial.size());
-    if (!c.spec.empty())
-      std::memcpy(slot + c.trial.size(), c.spec_pts.data(), sizeof(double) * c.spec.size() * 4 * (size_t)P);
+    if (c.nodes.empty())
+      std::memcpy(slot, c.trial.data(), sizeof(double) * c.trial.size());
+    else
+      std::memcpy(slot, c.pts.data(), sizeof(double) * c.nodes.size() * 4 * (size_t)P);
   };
   // group g: chains [r0[g], r0[g + 1]), slots [r0[g]Â·SLOT, r0[g + 1]Â·SLOT) of every buffer
-  int r0[3] = {0, G > 1 ? R / 2 : R, R};
-  bool pending[2] = {false, false};
+  int r0[kMaxGroups + 1];
+  for (int g = 0; g <= G; ++g) r0[g] = (int)((long long)R * g / G);
+  bool pending[kMaxGroups] = {};
   auto host_group = [&](int g) {
     active.store(0);
-    pool.run(r0[g + 1] - r0[g], 8, [&](int i) { host_step(r0[g] + i); });
+    pool.run(r0[g + 1] - r0[g], 2, [&](int i) { host_step(r0[g] + i); });
     return active.load() > 0;
   };
   auto submit = [&](int g) -> int {
@@ -683,10 +824,30 @@ extern "C" int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const
     evals += c.used;
     hits += c.spec_hits;
   }
-  if (stats)
+  if (stats) {
     std::fprintf(stderr, "yfm_estimate: %lld rounds, %lld chain evaluations, %lld device evaluations, %lld "
                  "speculated iterations used; host %.3f s, waiting on the device %.3f s (%d groups)\n", rounds, evals,
                  device_evals, hits, t_host, t_dev, G);
+    long long tr[8][8] = {}, dh[8] = {}, rc[2] = {};
+    for (const Chain& c : chains) {
+      for (int a = 0; a < 8; ++a) {
+        dh[a] += c.depth_hist[a];
+        for (int b = 0; b < 8; ++b) tr[a][b] += c.trans[a][b];
+      }
+      rc[0] += c.recent[0];
+      rc[1] += c.recent[1];
+    }
+    std::fprintf(stderr, "yfm_estimate: %d tree nodes per round; iterations per NM round:", spec_nodes);
+    for (int a = 1; a < 8; ++a) std::fprintf(stderr, " %d:%lld", a, dh[a]);
+    std::fprintf(stderr, "; worst = previously replaced vertex in %lld of %lld non-new outcomes\n", rc[0], rc[1]);
+    std::fprintf(stderr, "yfm_estimate: iteration outcome transitions (row: previous, col: next; "
+                 "R E O O* I I* S, * = new vertex is the worst; row 7 = first)\n");
+    for (int a = 0; a < 8; ++a) {
+      std::fprintf(stderr, "  %d:", a);
+      for (int b = 0; b < 7; ++b) std::fprintf(stderr, " %9lld", tr[a][b]);
+      std::fprintf(stderr, "\n");
+    }
+  }
   for (int r = 0; r < R; ++r) {
     const Chain& c = chains[r];
     const bool ok = c.status != 1;
