@@ -77,7 +77,11 @@ def main():
         out.update({"cpu_window": Tw, "cpu_seconds_one_task": cpu_s, "cpu_objective_evals": calls[0],
                     "cpu_threads": 1, "cpu_kind": "port (oracle/optim_nm.py + oracle/yfm_oracle.c)",
                     "gpu_vs_cpu_ll_rel": abs(r["ll"][k] - ref.ll) / abs(ref.ll),
-                    "speedup_per_task": cpu_s / (gpu_s / len(wins))})
+                    "speedup_per_task": cpu_s / (gpu_s / len(wins)),
+                    # like for like: the reference runs one task per process, so 16 host cores take
+                    # ≈ windows/16 of these tasks each (one mid-size window stands for the average)
+                    "cpu_16_processes_seconds_all_windows_est": cpu_s * len(wins) / 16,
+                    "speedup_vs_16_processes": cpu_s * len(wins) / 16 / gpu_s})
     print(json.dumps(out), flush=True)
 
 

@@ -1,7 +1,8 @@
 #!/bin/bash
 # One GPU-box pass over every BASELINE config: bench JSON, rocprofv3 kernel-trace stats,
 # and the PMC passes (one counter group per run, each under its own hard limit) for the
-# dominant kernel of configs 2, 3, 5.  Usage (repo root, via gpurun): bash tools/profile_all.sh [outdir]
+# dominant kernel of configs 2, 3, 5 (skipped with NOPMC=1), then the rolling re-estimation benchmark.
+# Usage (repo root, via gpurun): [NOPMC=1] bash tools/profile_all.sh [outdir]
 set -eo pipefail
 export TMPDIR=/tmp
 OUT=${1:-gpurun_out/prof_all}
@@ -18,6 +19,9 @@ pass() { c=$1; name=$2; shift 2
     python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-host-rate > "$OUT/pmc_c${c}_$name.log" 2>&1
   echo "pmc c$c $name ok"
 }
+timeout -k 10 300 python -u tools/bench_estimate.py > "$OUT/bench_estimate.json" 2> "$OUT/bench_estimate.err"
+echo "bench_estimate ok"
+[ -n "$NOPMC" ] && exit 0
 for c in 2 3 5; do
   pass $c fetch FETCH_SIZE
   pass $c write WRITE_SIZE

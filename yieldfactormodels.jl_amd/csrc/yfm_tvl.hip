@@ -280,6 +280,14 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
       const double u[M] = {s[U1], s[U2], s[U3], s[U4]};
       const double vv = s[VV];
 
+#if defined(YFM_TVL_PROBE) && YFM_TVL_PROBE == 1
+      // timing probe only (tools/build_probe.sh): the 4×4 update replaced by a data-dependent no-op
+      double det = 1.0 + 1e-300 * (vv + G[3][3]);
+#pragma unroll
+      for (int i = 0; i < M; ++i) beta[i] = fma(1e-300, u[i], beta[i]);
+      const bool upd = true;
+      const double q = vv * rsig2;
+#else
       double W[M][M], det;
       Capacitance<M>::solve(Pm, G, sigma2, W, det);
 #pragma unroll
@@ -302,6 +310,7 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
         for (int k = i; k < M; ++k) Pf[i][k] = sigma2 * W[i][k];
       const bool upd = det != 0.0;  // inv(F) threw: return without updating (filter.jl:51-56)
       if (upd) propagate_state<M, 0>(p, bf, Pf, beta, Pm);
+#endif
       last_det = det;
       last_q = upd ? q : __builtin_nan("");
       if (acc) {

@@ -555,6 +555,14 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
         vv = a.value();
       }
 
+#if defined(YFM_TVL_PROBE) && YFM_TVL_PROBE == 1
+      // timing probe only (tools/build_probe.sh): the 4×4 update replaced by a data-dependent no-op
+#pragma unroll
+      for (int i = 0; i < M4; ++i) beta[i] = dd_add(beta[i], dd_ldexp(u[i], -1000));
+      const double q = dd_to_double(dd_mul(vv, rsig2));
+      const double dh = 1.0 + 1e-300 * G[3][3].hi;
+      const bool upd = true;
+#else
       // ---- capacitance solve: B̃ = σ²I + P G, W = B̃⁻¹P ----
       dd A[M4][M4], W[M4][M4];
 #pragma unroll
@@ -590,6 +598,7 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
       const double dh = dd_to_double(det);
       const bool upd = dh != 0.0;  // inv(F) threw: return without updating (filter.jl:51-56)
       if (upd) dd_propagate(par, bf, Ws, true, beta, Pm);
+#endif
       last_ld = upd ? log(fabs(dh)) : -__builtin_inf();
       last_q = upd ? q : __builtin_nan("");
       last_neg = dh < 0.0;
