@@ -268,7 +268,7 @@ def pmc_executed_flops(kernel_substr: str):
     return None
 
 
-def pmc_traffic(kernel_substr: str):
+def pmc_traffic(kernel_substr: str, evals: int):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 --pmc passes
     (tools/profile_all.sh → profiles/<round>/**/pmc_summary.json), corrected as
     MI355X_MICROARCH.md §HBM prescribes for gfx950: FETCH_SIZE counts half the bytes of wide
@@ -276,7 +276,8 @@ def pmc_traffic(kernel_substr: str):
     for rnd in sorted((ROOT / "profiles").glob("r*/**/pmc_summary.json"), reverse=True):
         d = json.loads(rnd.read_text())
         for k, v in d.items():
-            if kernel_substr in k and "FETCH_SIZE" in v and "WRITE_SIZE" in v:
+            if kernel_substr in k and "FETCH_SIZE" in v and "WRITE_SIZE" in v and \
+                    int(v.get("evals_per_launch", evals)) == int(evals):  # the same launch size only
                 return (2.0 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024.0, str(rnd.relative_to(ROOT))
     return None, None
 
@@ -293,7 +294,7 @@ def roofline(kind, prec, N, M, T, T_use, B, P, kernel_ms):
     f_survey = float(np.sum(alg_flops(kind, N, M, Tb, survey_flops_step)))
     achieved = f_rank / (kernel_ms * 1e-3) / 1e12
     name = DOMINANT[(kind, prec)] if kind == KIND_TVL else DOMINANT[kind]
-    traffic, traffic_src = pmc_traffic(name)
+    traffic, traffic_src = pmc_traffic(name, B)
     exe = pmc_executed_flops(name)
     steps = float(np.sum(Tb - 1))
     exe_tf = exe * steps / (kernel_ms * 1e-3) / 1e12 if exe else None

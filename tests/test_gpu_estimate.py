@@ -174,3 +174,29 @@ def test_speculation_is_bitwise_neutral(engine, panel):
         for k in ("theta_c", "p", "init_c", "ll", "status"):
             np.testing.assert_array_equal(a[k], b[k], err_msg=f"{k} at {mode} nodes")
         assert a["n_evals"] == b["n_evals"]
+
+
+@pytest.mark.parametrize("kind_name", ["GNS5", "TVL"])
+def test_speculation_tree_other_models(engine, panel, kind_name):
+    """The speculation tree on the larger simplices (GNS5: 48 parameters, TVλ: 31, certified
+    precision): budgets 1 and 16 give the same chains bit for bit and the same evaluation count."""
+    import os
+    from yfm_amd import KIND_GNS, KIND_TVL
+    kind = {"GNS5": KIND_GNS, "TVL": KIND_TVL}[kind_name]
+    Y, mats = panel
+    Y = Y[:, :40].copy(order="F")
+    engine.set_panel(Y, mats)
+    starts = S.theta_batch(kind, 3, seed=71, bad_frac=0.0, scale=0.05)
+    win = np.array([40, 33, 25], dtype=np.int32)
+    res = {}
+    for mode in ("1", "16"):
+        os.environ["YFM_NM_SPEC"] = mode
+        try:
+            res[mode] = engine.estimate(kind, starts, space=0, T_use=win, iterations=40, max_group_iters=2)
+        finally:
+            os.environ.pop("YFM_NM_SPEC", None)
+    a, b = res["1"], res["16"]
+    for k in ("theta_c", "p", "init_c", "ll", "status"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    assert a["n_evals"] == b["n_evals"] and a["n_evals"] > 0
+    assert np.isfinite(a["ll"]).all()
