@@ -1,4 +1,8 @@
-"""GPU tests at the full workloads of BASELINE.json configs 4 and 5.
+"""GPU tests at the full workloads of BASELINE.json configs 2, 4 and 5.
+
+Config 2 — the headline batch (bench.py's 65,536 θ, DNS, T = 600, N = 30): every candidate vs
+the dense C oracle; every one more than 1e-9 from it adjudicated at factor 1 by the binary128
+truth (not just a sample).
 
 Config 4 — rolling re-estimation (forecasting.jl:86, :140-158): 240 expanding windows
 T_w = 361..600 of the T = 600 panel × 4,096 θ per window = 983,040 evaluations in one
@@ -26,6 +30,24 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(scope="module")
 def dns_panel():
     return S.simulate_panel(KIND_DNS, 600), S.maturities_30()
+
+
+def test_config2_whole_batch_adjudicated(engine, dns_panel):
+    Y, mats = dns_panel
+    B = 65536
+    Th = S.theta_batch(KIND_DNS, B)  # bench.py's config-2 batch
+    engine.set_panel(Y, mats)
+    got = engine.loglik(KIND_DNS, Th)
+    ora = loglik_oracle(KIND_DNS, Y, mats, Th)
+    assert np.array_equal(np.isnan(got), np.isnan(ora)) and np.array_equal(np.isneginf(got), np.isneginf(ora))
+    fin = np.isfinite(ora)
+    err = np.zeros(B)
+    err[fin] = np.abs(got[fin] - ora[fin]) / np.abs(ora[fin])
+    far = np.flatnonzero(fin & (err > 1e-9))
+    assert len(far) <= B // 100, len(far)
+    table = assert_parity(got[far], ora[far], loglik_truth(KIND_DNS, Y, mats, Th[:, far]))
+    print(f"config 2 whole batch: {int(fin.sum())} finite, {int(fin.sum()) - len(far)} within 1e-9, far ones:",
+          table)
 
 
 def test_config4_windows_full_workload(engine, dns_panel):
