@@ -274,11 +274,16 @@ void build_tree(Chain& c, int budget, int max_depth) {
   // P(next kind | previous kind) from the chain's counts plus one pseudo-count per kind;
   // rq: share of "not the new vertex" outcomes whose worst is the previously replaced vertex
   double pk[8][7];
-  for (int a = 0; a < 8; ++a) {
-    double s = 0.0;
-    for (int b = 0; b < 7; ++b) s += (double)c.trans[a][b] + 1.0;
-    for (int b = 0; b < 7; ++b) pk[a][b] = ((double)c.trans[a][b] + 1.0) / s;
-  }
+  bool pk_ok[8] = {};
+  auto row_of = [&](int a) -> const double* {
+    if (!pk_ok[a]) {
+      double t = 0.0;
+      for (int k = 0; k < 7; ++k) t += (double)c.trans[a][k] + 1.0;
+      for (int k = 0; k < 7; ++k) pk[a][k] = ((double)c.trans[a][k] + 1.0) / t;
+      pk_ok[a] = true;
+    }
+    return pk[a];
+  };
   const double rq = ((double)c.recent[0] + 1.0) / ((double)c.recent[1] + 2.0);
   struct Cand {
     int parent, src, h, kind;
@@ -287,27 +292,27 @@ void build_tree(Chain& c, int budget, int max_depth) {
   Cand cand[kMaxNodes * 4 * 8];  // a max-heap on prob
   int nc = 0;
   auto by_prob = [](const Cand& a, const Cand& b) { return a.prob < b.prob; };
-  unsigned char mark[kMaxSlot];
   auto expand = [&](int x) {
     const Chain::Node X = c.nodes[x];
     if (X.depth >= max_depth) return;
-    std::memset(mark, 0, (size_t)m);
-    int nu = 0;  // vertices replaced on the path to X, other than h_X
+    int uu[kMaxNodes];  // the vertices replaced on the path to X other than h_X (values unknown)
+    int nu = 0;
     for (int p = x; c.nodes[p].parent >= 0; p = c.nodes[p].parent) {
       const int u = c.nodes[c.nodes[p].parent].h;
-      if (u != X.h && !mark[u]) ++nu;
-      mark[u] = 1;
+      bool seen = u == X.h;
+      for (int q = 0; q < nu && !seen; ++q) seen = uu[q] == u;
+      if (!seen) uu[nu++] = u;
     }
-    mark[X.h] = 1;
     int wk = -1;  // the worst vertex with a known value
-    for (int i = n; i >= 0; --i)
-      if (!mark[c.order[i]]) {
-        wk = c.order[i];
-        break;
-      }
-    const double* row = pk[X.kind];
+    for (int i = n; i >= 0 && wk < 0; --i) {
+      const int v = c.order[i];
+      bool rep = v == X.h;
+      for (int q = 0; q < nu && !rep; ++q) rep = uu[q] == v;
+      if (!rep) wk = v;
+    }
+    const double* row = row_of(X.kind);
     auto push = [&](int src, int h, int kind, double p) {
-      if (p < 1e-4 || nc >= (int)(sizeof(cand) / sizeof(cand[0]))) return;
+      if (p < 5e-3 || nc >= (int)(sizeof(cand) / sizeof(cand[0]))) return;  // never among the top nodes
       cand[nc++] = {x, src, h, kind, p};
       std::push_heap(cand, cand + nc, by_prob);
     };
@@ -316,9 +321,7 @@ void build_tree(Chain& c, int budget, int max_depth) {
       if (src >= 2) push(src, X.h, kn + 1, X.prob * row[kn + 1]);
       const double pn = X.prob * row[kn];
       if (wk >= 0) push(src, wk, kn, pn * (nu ? 1.0 - rq : 1.0));
-      if (nu)
-        for (int u = 0; u < m; ++u)
-          if (mark[u] && u != X.h) push(src, u, kn, pn * rq / nu);
+      for (int q = 0; q < nu; ++q) push(src, uu[q], kn, pn * rq / nu);
     }
   };
   expand(0);
@@ -399,6 +402,7 @@ class Pool {
     {
       std::lock_guard<std::mutex> g(m_);
       stop_ = true;
+      stop_a_.store(true, std::memory_order_release);
     }
     cv_.notify_all();
     for (auto& t : th_) t.join();
@@ -411,6 +415,7 @@ class Pool {
       return;
     }
     std::function<void(int)> job = [&](int i) { f(i); };
+    bool wake;
     {
       std::lock_guard<std::mutex> g(m_);
       job_ = &job;
@@ -419,10 +424,12 @@ class Pool {
       next_.store(0);
       done_.store(0);
       ++gen_;
+      gen_a_.store(gen_, std::memory_order_release);
+      wake = sleepers_ > 0;
     }
-    cv_.notify_all();
+    if (wake) cv_.notify_all();
     drain();
-    while (done_.load(std::memory_order_acquire) < n) std::this_thread::yield();
+    while (done_.load(std::memory_order_acquire) < n) __builtin_ia32_pause();
     std::lock_guard<std::mutex> g(m_);
     job_ = nullptr;
   }
@@ -437,14 +444,30 @@ class Pool {
       done_.fetch_add(i1 - i0, std::memory_order_release);
     }
   }
+  // Rounds come every few hundred µs: a worker spins for the next one (a futex wake-up costs tens
+  // of µs per thread) and only sleeps after 2 ms without work.
   void worker() {
     int seen = 0;
     for (;;) {
-      std::unique_lock<std::mutex> lk(m_);
-      cv_.wait(lk, [&] { return stop_ || (gen_ != seen && job_); });
-      if (stop_) return;
-      seen = gen_;
-      lk.unlock();
+      const auto t0 = std::chrono::steady_clock::now();
+      for (int k = 0; gen_a_.load(std::memory_order_acquire) == seen && !stop_a_.load(std::memory_order_acquire); ++k) {
+        __builtin_ia32_pause();
+        if ((k & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+      }
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        if (!stop_ && gen_ == seen) {
+          ++sleepers_;
+          cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+          --sleepers_;
+        }
+        if (stop_) return;
+        if (!job_) {  // the round this generation announced is already over
+          seen = gen_;
+          continue;
+        }
+        seen = gen_;
+      }
       drain();
     }
   }
@@ -452,9 +475,10 @@ class Pool {
   std::mutex m_;
   std::condition_variable cv_;
   std::function<void(int)>* job_ = nullptr;
-  int n_ = 0, chunk_ = 1, gen_ = 0;
+  int n_ = 0, chunk_ = 1, gen_ = 0, sleepers_ = 0;
   bool stop_ = false;
-  std::atomic<int> next_{0}, done_{0};
+  std::atomic<int> next_{0}, done_{0}, gen_a_{0};
+  std::atomic<bool> stop_a_{false};
 };
 
 // objective values −loglik of this chain's requests; NaN ⇔ compute_loss threw
@@ -706,8 +730,10 @@ extern "C" int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const
   long long device_evals = 0, rounds = 0;
   double t_host = 0.0, t_dev = 0.0;
   using clk = std::chrono::steady_clock;
+  std::atomic<long long> ns_consume{0}, ns_prepare{0}, ns_copy{0};  // host time split (YFM_EST_STATS)
   auto host_step = [&](int r) {
     Chain& c = chains[r];
+    const auto h0 = stats ? clk::now() : clk::time_point();
     if (c.n_req > 0) {  // the results of this chain's slot from the last round
       double f[kMaxSlot];
       const int nv = c.nodes.empty() ? c.n_req : 4 * (int)c.nodes.size();
@@ -754,14 +780,23 @@ extern "C" int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const
       }
       c.nodes.clear();
     }
+    const auto h1 = stats ? clk::now() : clk::time_point();
     prepare(c, iterations, spec_nodes);
-    if (c.n_req == 0) return;
-    active.fetch_add(1, std::memory_order_relaxed);
-    double* slot = th + (size_t)r * SLOT * P;
-    if (c.nodes.empty())
-      std::memcpy(slot, c.trial.data(), sizeof(double) * c.trial.size());
-    else
-      std::memcpy(slot, c.pts.data(), sizeof(double) * c.nodes.size() * 4 * (size_t)P);
+    const auto h2 = stats ? clk::now() : clk::time_point();
+    if (c.n_req > 0) {
+      active.fetch_add(1, std::memory_order_relaxed);
+      double* slot = th + (size_t)r * SLOT * P;
+      if (c.nodes.empty())
+        std::memcpy(slot, c.trial.data(), sizeof(double) * c.trial.size());
+      else
+        std::memcpy(slot, c.pts.data(), sizeof(double) * c.nodes.size() * 4 * (size_t)P);
+    }
+    if (stats) {
+      const auto h3 = clk::now();
+      ns_consume += std::chrono::duration_cast<std::chrono::nanoseconds>(h1 - h0).count();
+      ns_prepare += std::chrono::duration_cast<std::chrono::nanoseconds>(h2 - h1).count();
+      ns_copy += std::chrono::duration_cast<std::chrono::nanoseconds>(h3 - h2).count();
+    }
   };
   // group g: chains [r0[g], r0[g + 1]), slots [r0[g]·SLOT, r0[g + 1]·SLOT) of every buffer
   int r0[kMaxGroups + 1];
@@ -837,6 +872,9 @@ extern "C" int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const
       rc[0] += c.recent[0];
       rc[1] += c.recent[1];
     }
+    std::fprintf(stderr, "yfm_estimate: host thread time: consume + tree walk %.3f s, prepare %.3f s, slot copy %.3f s "
+                 "(%d threads)\n", ns_consume.load() * 1e-9, ns_prepare.load() * 1e-9, ns_copy.load() * 1e-9,
+                 std::min(nthreads, std::max(1, R / (4 * G))));
     std::fprintf(stderr, "yfm_estimate: %d tree nodes per round; iterations per NM round:", spec_nodes);
     for (int a = 1; a < 8; ++a) std::fprintf(stderr, " %d:%lld", a, dh[a]);
     std::fprintf(stderr, "; worst = previously replaced vertex in %lld of %lld non-new outcomes\n", rc[0], rc[1]);
