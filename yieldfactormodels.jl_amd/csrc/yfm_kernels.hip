@@ -461,21 +461,26 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
       read_z(0, zc);
       double2 yb = *reinterpret_cast<const double2*>(cb + NP);
       double2 meta = *reinterpret_cast<const double2*>(cb + NP + 2);
-      for (int tt = 0; tt < tend; ++tt) {
+      // two steps per trip with the operand buffers swapped by name (no register copies)
+      double zn[NZ];
+      double2 ybn, metan;
+      auto half = [&](int tt, const double (&zc_)[NZ], double2 yb_, double2 meta_, double (&zn_)[NZ], double2& ybn_,
+                      double2& metan_) {
         const int t = t0 + tt;
         const int tn = min(tt + 1, TB - 1);
-        double zn[NZ];
-        read_z(tn, zn);
-        const double2 ybn = *reinterpret_cast<const double2*>(cb + tn * LDP + NP);
-        const double2 metan = *reinterpret_cast<const double2*>(cb + tn * LDP + NP + 2);
-        do_step(t, zc, yb, meta);
+        read_z(tn, zn_);
+        ybn_ = *reinterpret_cast<const double2*>(cb + tn * LDP + NP);
+        metan_ = *reinterpret_cast<const double2*>(cb + tn * LDP + NP + 2);
+        do_step(t, zc_, yb_, meta_);
         record(t);
         rotate(t);
-#pragma unroll
-        for (int j = 0; j < NZ; ++j) zc[j] = zn[j];
-        yb = ybn;
-        meta = metan;
+      };
+      int tt = 0;
+      for (; tt + 1 < tend; tt += 2) {
+        half(tt, zc, yb, meta, zn, ybn, metan);
+        half(tt + 1, zn, ybn, metan, zc, yb, meta);
       }
+      if (tt < tend) half(tt, zc, yb, meta, zn, ybn, metan);
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();  // scratch reads done before the next block's writes
     }
@@ -488,20 +493,25 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
       yb_c = *reinterpret_cast<const double2*>(c0 + NP);
       meta_c = *reinterpret_cast<const double2*>(c0 + NP + 2);
     }
-    for (int t = 0; t < nsteps; ++t) {
+    // two steps per trip with the operand buffers swapped by name (as in the MFMA path)
+    double zn[NZ];
+    double2 yb_n, meta_n;
+    auto half = [&](int t, const double (&zc_)[NZ], double2 yb_, double2 meta_, double (&zn_)[NZ], double2& ybn_,
+                    double2& metan_) {
       const double* cn = col_of(t + 1);  // t + 1 ≤ nsteps ≤ T − 1: a resident panel column
-      double zn[NZ];
-      dot_zt<NP, NZ>(cn, Zc, zn);
-      const double2 yb_n = *reinterpret_cast<const double2*>(cn + NP);
-      const double2 meta_n = *reinterpret_cast<const double2*>(cn + NP + 2);
-      do_step(t, zc, yb_c, meta_c);
+      dot_zt<NP, NZ>(cn, Zc, zn_);
+      ybn_ = *reinterpret_cast<const double2*>(cn + NP);
+      metan_ = *reinterpret_cast<const double2*>(cn + NP + 2);
+      do_step(t, zc_, yb_, meta_);
       record(t);
-#pragma unroll
-      for (int j = 0; j < NZ; ++j) zc[j] = zn[j];
-      yb_c = yb_n;
-      meta_c = meta_n;
       rotate(t);
+    };
+    int t = 0;
+    for (; t + 1 < nsteps; t += 2) {
+      half(t, zc, yb_c, meta_c, zn, yb_n, meta_n);
+      half(t + 1, zn, yb_n, meta_n, zc, yb_c, meta_c);
     }
+    if (t < nsteps) half(t, zc, yb_c, meta_c, zn, yb_n, meta_n);
   }
 
   if (!live || defer) return;
