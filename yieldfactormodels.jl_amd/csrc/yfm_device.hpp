@@ -464,8 +464,8 @@ __device__ __forceinline__ double group_level_sum(double x) {
   if constexpr (LVL == 0 || LVL == 1 || LVL == 2 || LVL == 3) {
     // quad_perm xor1 / xor2, row_half_mirror, row_mirror
     constexpr int ctrl = LVL == 0 ? 0xB1 : LVL == 1 ? 0x4E : LVL == 2 ? 0x141 : 0x140;
-    const int plo = __builtin_amdgcn_update_dpp(0, lo, ctrl, 0xf, 0xf, false);
-    const int phi = __builtin_amdgcn_update_dpp(0, hi, ctrl, 0xf, 0xf, false);
+    const int plo = __builtin_amdgcn_mov_dpp(lo, ctrl, 0xf, 0xf, true);
+    const int phi = __builtin_amdgcn_mov_dpp(hi, ctrl, 0xf, 0xf, true);
     return x + __hiloint2double(phi, plo);
   } else if constexpr (LVL == 4) {
     // rows (0,1), (2,3): vdst' = [r0 r0 r2 r2], src' = [r1 r1 r3 r3]

@@ -137,8 +137,8 @@ __device__ __forceinline__ void pair_exchange(double x, double& a, double& b) {
   const int lo = __double2loint(x), hi = __double2hiint(x);
   if constexpr (LVL <= 3) {
     constexpr int ctrl = LVL == 0 ? 0xB1 : LVL == 1 ? 0x4E : LVL == 2 ? 0x141 : 0x140;
-    const int plo = __builtin_amdgcn_update_dpp(0, lo, ctrl, 0xf, 0xf, false);
-    const int phi = __builtin_amdgcn_update_dpp(0, hi, ctrl, 0xf, 0xf, false);
+    const int plo = __builtin_amdgcn_mov_dpp(lo, ctrl, 0xf, 0xf, true);
+    const int phi = __builtin_amdgcn_mov_dpp(hi, ctrl, 0xf, 0xf, true);
     const double p = __hiloint2double(phi, plo);
     // canonical order (lower lane's value first) so both partners compute the same bits
     const bool lower = LVL == 0 ? !(threadIdx.x & 1) : LVL == 1 ? !(threadIdx.x & 2)
