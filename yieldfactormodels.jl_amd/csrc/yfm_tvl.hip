@@ -148,6 +148,9 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
   double sumq = 0.0;
   bool neg = false;
   double last_det = 0.0, last_q = 0.0;  // fresh model: F = 0, F⁻¹ = 0, v = 0 (kalmanbasemodel.jl:65-67)
+#if defined(YFM_TVL_PROBE) && YFM_TVL_PROBE == 2
+  bool probe_swapped = false;  // statistics probe: did partial pivoting ever exchange rows?
+#endif
 
   __syncthreads();
   const int nsteps = max(s_nobs_max, 0);
@@ -289,7 +292,11 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
       const double q = vv * rsig2;
 #else
       double W[M][M], det;
+#if defined(YFM_TVL_PROBE) && YFM_TVL_PROBE == 2
+      Capacitance<M>::solve(Pm, G, sigma2, W, det, &probe_swapped);  // statistics probe
+#else
       Capacitance<M>::solve(Pm, G, sigma2, W, det);
+#endif
 #pragma unroll
       for (int i = 0; i < M; ++i)
 #pragma unroll
@@ -342,6 +349,9 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
   }
 
   if (!live || j != 0) return;
+#if defined(YFM_TVL_PROBE) && YFM_TVL_PROBE == 2
+  if (probe_swapped) atomicAdd(&flags[0], 1u);  // statistics probe: filters that ever pivoted
+#endif
   double ll;
   if (!init_ok) {
     ll = __builtin_nan("");  // the reference throws from initialize_filter
