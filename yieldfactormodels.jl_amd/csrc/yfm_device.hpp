@@ -296,6 +296,13 @@ __device__ __forceinline__ double rcp_nr(double d) {
   return fma(r, e, r);
 }
 
+// 1/d from v_rcp_f64 and ONE Newton step (the seed's error squared: ≈ 1 ulp), for the per-step
+// LDLᵀ pivots of the fixed-loading filter, where the reciprocal sits on the serial chain
+__device__ __forceinline__ double rcp_nr1(double d) {
+  const double r = __builtin_amdgcn_rcp(d);
+  return fma(r, fma(-d, r, 1.0), r);
+}
+
 // Symmetric LDLᵀ (no pivoting) of an M×M matrix S, solving S X = Rhs in place for
 // R right-hand sides; returns det S = ∏ d_i (its sign is exact in the factorised
 // arithmetic).  Used on S = P + σ²(Z'Z)⁻¹, which is SPD whenever P is PSD.
@@ -360,7 +367,7 @@ struct LDLT {
 #pragma unroll
       for (int k = 0; k < j; ++k) dj = fma(-a[j][k], L[j][k], dj);
       d[j] = dj;
-      rd[j] = rcp_nr(dj);
+      rd[j] = rcp_nr1(dj);
 #pragma unroll
       for (int i = j + 1; i < M; ++i) {
         double s = S[i][j];
