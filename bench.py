@@ -257,13 +257,14 @@ def cpu_baseline(w: Workload, seconds: float, gpu_out: np.ndarray):
     return out
 
 
-def pmc_executed_flops(kernel_substr: str):
+def pmc_executed_flops(kernel_substr: str, evals: int):
     """Executed FP64 flops per filter step of the dominant kernel from the committed PMC valu pass (T = 600):
     (FMA·2 + ADD + MUL)·64 + MFMA_MOPS_F64·512 (the expression of rocprof's SQ_INSTS_VALU_FLOPS_FP64)."""
     for rnd in sorted((ROOT / "profiles").glob("r*/**/pmc_summary.json"), reverse=True):
         d = json.loads(rnd.read_text())
         for k, v in d.items():
-            if kernel_substr in k and "fp64_flops_executed_per_step" in v:
+            if kernel_substr in k and "fp64_flops_executed_per_step" in v and \
+                    int(v.get("evals_per_launch", evals)) == int(evals):  # the same launch size only
                 return v["fp64_flops_executed_per_step"]
     return None
 
@@ -295,7 +296,7 @@ def roofline(kind, prec, N, M, T, T_use, B, P, kernel_ms):
     achieved = f_rank / (kernel_ms * 1e-3) / 1e12
     name = DOMINANT[(kind, prec)] if kind == KIND_TVL else DOMINANT[kind]
     traffic, traffic_src = pmc_traffic(name, B)
-    exe = pmc_executed_flops(name)
+    exe = pmc_executed_flops(name, B)
     steps = float(np.sum(Tb - 1))
     exe_tf = exe * steps / (kernel_ms * 1e-3) / 1e12 if exe else None
     return {"bound": "fp64-valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
