@@ -12,6 +12,7 @@ default certified precision).  −Inf / NaN patterns must match exactly."""
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -67,7 +68,7 @@ def random_case(rng, kind):
     return N, T, mats, Y, Th, space, T_use
 
 
-@pytest.mark.parametrize("seed", range(12))
+@pytest.mark.parametrize("seed", range(int(os.environ.get("YFM_RANDOM_SEEDS", "12"))))  # a wider sweep on demand
 def test_random_cases_vs_c_oracle(engine, seed):
     rng = np.random.default_rng(1000 + seed)
     kind = [KIND_DNS, KIND_GNS, KIND_TVL][seed % 3]
@@ -78,9 +79,15 @@ def test_random_cases_vs_c_oracle(engine, seed):
     ref = c_oracle(kind, space, Y, mats, Th, T_use)
     what = dict(kind=kind, N=N, T=T, space=space, windows=T_use is not None)
     assert np.array_equal(np.isnan(got), np.isnan(ref)), what
-    assert np.array_equal(np.isneginf(got), np.isneginf(ref)), (what, got, ref)
     assert not np.isposinf(got).any()
-    fin = np.isfinite(ref)
+    truth = loglik_truth(kind, Y, mats, Th, space=space, T_use=T_use)
+    # −Inf patterns: exact, unless the oracle's FP64 dense determinant has the wrong sign — then the
+    # kernel must agree with the binary128 truth (factor-1 adjudication applied to the pattern)
+    for b in np.flatnonzero(np.isneginf(got) != np.isneginf(ref)):
+        assert np.isneginf(truth[b]) == np.isneginf(got[b]), (what, b, got[b], ref[b], truth[b])
+        if np.isfinite(got[b]):
+            assert abs(got[b] - truth[b]) <= 1e-9 * abs(truth[b]), (what, b, got[b], truth[b])
+    fin = np.isfinite(ref) & np.isfinite(got)
     # error scale: the loglik is a sum of per-step terms −½(log det F + v'F⁻¹v + N log 2π); FP64
     # accuracy is relative to the terms' magnitude, not to a sum that may cancel to ≈ 0 (random
     # short panels do that): scale = max(|ll|, ½·nterms·N·log 2π)
@@ -89,7 +96,6 @@ def test_random_cases_vs_c_oracle(engine, seed):
     err = np.zeros_like(ref)
     err[fin] = np.abs(got[fin] - ref[fin]) / np.maximum(scale[fin], 1e-300)
     assert np.all((ref[fin] != 0.0) | (got[fin] == 0.0)), what  # loglik exactly 0 (T_use ≤ 2) is exact
-    truth = loglik_truth(kind, Y, mats, Th, space=space, T_use=T_use)
     for b in np.flatnonzero(fin & (err > 1e-9)):
         e_gt = abs(got[b] - truth[b]) / max(abs(truth[b]), scale[b])
         e_or = abs(ref[b] - truth[b]) / max(abs(truth[b]), scale[b])

@@ -211,8 +211,13 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
       const double lam = 1e-2 + exp(beta[3]);  // tvλdns.jl:56
       const double rl = 1.0 / lam;
       const double dl = lam - 1e-2;            // filter.jl:38
-      const double c1 = (beta[1] + beta[2]) * dl;
-      const double c2 = beta[2] * dl;
+      // λ near the FP64 range (c1 or c2 overflows): every z = e^{−λm} underflows to 0 and the
+      // reference's Jacobian column is ((β2+β3)·0 + β3·0)·dλ = 0·dλ (0, or NaN for dλ = Inf), so the
+      // factored form's constants become 0·dλ instead of multiplying z = 0 by an Inf
+      const double c1r = (beta[1] + beta[2]) * dl, c2r = beta[2] * dl;
+      const bool big = !(fabs(c1r) <= __DBL_MAX__) || !(fabs(c2r) <= __DBL_MAX__);
+      const double c1 = big ? 0.0 * dl : c1r;
+      const double c2 = big ? 0.0 * dl : c2r;
       const double k1 = c1 * rl;
       const double* col = s_y + tt * N;
       double s[NSTAT];

@@ -38,6 +38,13 @@ constexpr int M4 = 4;
 // reading their own table hit disjoint banks (a 128 B stride is a 4-way conflict)
 constexpr int kDdWStride = kTvlGaps + 1;
 
+// −λ·m in dd for exp(−λm); a product that overflows (λ near the FP64 range) is −Inf, whose exp is
+// 0 as in the reference — TwoProd's error term would be Inf − Inf = NaN there
+__device__ __forceinline__ dd neg_rate(dd lam, double m) {
+  const dd p = dd_mul_d(lam, m);
+  return __builtin_isfinite(p.hi) ? dd_neg(p) : dd{-(lam.hi * m), 0.0};
+}
+
 // per-candidate record written by tvl_dd_init_kernel (doubles)
 constexpr int kDSig = 0;     // σ² (dd)
 constexpr int kDDelta = 2;   // δ (4 doubles, exact θ entries)
@@ -458,8 +465,13 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
       const dd lam = dd_add_d(e4, 1e-2);
       const dd dl = dd_add_d(lam, -1e-2);
       const dd rl = dd_rcp(lam);
-      const dd c1 = dd_mul(dd_add(beta[1], beta[2]), dl);
-      const dd c2 = dd_mul(beta[2], dl);
+      // λ near the FP64 range: every z underflows to 0 and the reference's Jacobian column is 0·dλ
+      // (yfm_tvl.hip) — the constants become 0·dλ rather than overflowed (Inf, NaN) pairs
+      const dd c1r = dd_mul(dd_add(beta[1], beta[2]), dl), c2r = dd_mul(beta[2], dl);
+      const bool big = !(fabs(c1r.hi) <= __DBL_MAX__) || !(fabs(c2r.hi) <= __DBL_MAX__) ||
+                       !(fabs(c1r.lo) <= __DBL_MAX__) || !(fabs(c2r.lo) <= __DBL_MAX__);
+      const dd c1 = big ? dd_make(0.0 * dl.hi) : c1r;
+      const dd c2 = big ? dd_make(0.0 * dl.hi) : c2r;
       const dd k1 = dd_mul(c1, rl);
       const double* col = s_y + tt * N;
       const dd kr = dd_mul(k1, rl);
@@ -500,18 +512,18 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
       };
       if (K > 0) {
         dd* w = s_w + grp * kDdWStride;
-        for (int q = j; q < K; q += L) w[q] = dd_exp(dd_neg(dd_mul_d(lam, s_gd[q])));
+        for (int q = j; q < K; q += L) w[q] = dd_exp(neg_rate(lam, s_gd[q]));
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        dd z = (j < N) ? dd_exp(dd_neg(dd_mul_d(lam, s_m[j]))) : dd_make(0.0);
+        dd z = (j < N) ? dd_exp(neg_rate(lam, s_m[j])) : dd_make(0.0);
         for (int i = j; i < N; i += L) {
           const dd wn = w[s_gi[i]];
           accum(i, z);
           z = dd_mul(z, wn);
         }
       } else {
-        for (int i = j; i < N; i += L) accum(i, dd_exp(dd_neg(dd_mul_d(lam, s_m[i]))));
+        for (int i = j; i < N; i += L) accum(i, dd_exp(neg_rate(lam, s_m[i])));
       }
       const dd s2 = group_sum_acc<L>(S2), sz = group_sum_acc<L>(Sz), s4 = group_sum_acc<L>(S4);
       const dd g22 = group_sum_acc<L>(G22), g2z = group_sum_acc<L>(G2z), g24 = group_sum_acc<L>(G24);
