@@ -468,8 +468,7 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
       // λ near the FP64 range: every z underflows to 0 and the reference's Jacobian column is 0·dλ
       // (yfm_tvl.hip) — the constants become 0·dλ rather than overflowed (Inf, NaN) pairs
       const dd c1r = dd_mul(dd_add(beta[1], beta[2]), dl), c2r = dd_mul(beta[2], dl);
-      const bool big = !(fabs(c1r.hi) <= __DBL_MAX__) || !(fabs(c2r.hi) <= __DBL_MAX__) ||
-                       !(fabs(c1r.lo) <= __DBL_MAX__) || !(fabs(c2r.lo) <= __DBL_MAX__);
+      const bool big = !(fabs(c1r.hi) <= __DBL_MAX__) || !(fabs(c2r.hi) <= __DBL_MAX__);
       const dd c1 = big ? dd_make(0.0 * dl.hi) : c1r;
       const dd c2 = big ? dd_make(0.0 * dl.hi) : c2r;
       const dd k1 = dd_mul(c1, rl);
