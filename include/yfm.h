@@ -184,6 +184,13 @@ int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const double* th
  * For yfm_loglik_batch_device, synchronise the stream first. */
 int yfm_last_batch_flags(yfm_ctx* ctx, long long* n_init_throw, long long* n_neg_inf);
 
+/* Candidates of the last completed batch on this ctx that the fixed-loading models (DNS, GNS5)
+ * evaluated on the double-double capacitance path instead of the FP64 collapsed form: an
+ * ill-conditioned loading Gram matrix (κ₁(Z'Z) ≥ 1e6), a singular one, or fewer maturities than
+ * states.  Same filter!/get_loss semantics (filter.jl:125-209); reported for auditing the cost
+ * and accuracy split (0 for TVλ).  For yfm_loglik_batch_device, synchronise the stream first. */
+int yfm_last_batch_deferred(yfm_ctx* ctx, long long* n_deferred);
+
 #ifdef __cplusplus
 }
 #endif

@@ -200,3 +200,50 @@ def test_speculation_tree_other_models(engine, panel, kind_name):
         np.testing.assert_array_equal(a[k], b[k], err_msg=k)
     assert a["n_evals"] == b["n_evals"] and a["n_evals"] > 0
     assert np.isfinite(a["ll"]).all()
+
+
+def test_rolling_forecasts_driver(engine, tmp_path):
+    """run_rolling_forecasts (forecasting.jl:16-51, :81-224) for "both" window types, single process:
+    the batched per-task estimation equals each task's chain run alone, the forecast records equal
+    the oracle's predict on hcat(window, NaN × (h−1)) rounded to 3 digits (databaseoperations.jl:
+    251-255), and the six export CSVs per window type have the reference's names and layouts
+    (databaseoperations.jl:391-661).  (tests/test_gpu_multirank.py checks that 2 ranks give the
+    same files; this test pins those files to the reference's semantics.)"""
+    from oracle import kalman_oracle as O
+    from yfm_amd import create_model
+    from yfm_amd import io as yio
+    from yfm_amd.forecasting import run_rolling_forecasts
+    mats = S.maturities_30()
+    Y = S.simulate_panel(KIND_DNS, 600)[:, :56].copy(order="F")
+    model, _ = create_model("1C", mats, 30, results_location=str(tmp_path) + "/")
+    th0 = S.theta0_constrained(KIND_DNS)
+    h = 3
+    out = run_rolling_forecasts(model, Y, "9", 50, 11, h, th0[:, None], window_type="both", max_group_iters=1,
+                                iterations=25)
+    ex, mv = out["expanding"], out["moving"]
+    tasks = np.arange(50, 57)
+    np.testing.assert_array_equal(ex["tasks"], tasks)
+    np.testing.assert_array_equal(ex["params"], mv["params"])  # both use the expanding sample (:165)
+    engine.set_panel(Y, mats)  # the moving-window forecasts left a window panel on the engine
+    one = engine.estimate(KIND_DNS, th0, space=1, T_use=[53], iterations=25, max_group_iters=1)
+    np.testing.assert_array_equal(one["theta_c"][:, 0], ex["params"][:, 3])
+    assert one["ll"][0] == ex["loss"][3]
+    for i, task in enumerate(tasks):
+        for wt, res, lo in (("expanding", ex, 0), ("moving", mv, task - 39 - 1)):
+            s = O.KalmanState.fresh(KIND_DNS, mats, 3)
+            O.set_params(s, res["params"][:, i])
+            r = O.predict(s, O.pad_nan(Y[:, lo:task], h))
+            for k in ("preds", "factors", "factor_loadings_1"):
+                ref = yio.julia_round(r[k][:, -h:], 3)
+                assert np.abs(res[k][:, :, i] - ref).max() <= 1.0001e-3, (wt, k, task)
+                assert (res[k][:, :, i] == ref).mean() > 0.9
+    for wt in ("expanding", "moving"):
+        f = yio.readdlm(tmp_path / f"1C__thread_id__9__{wt}_window_forecasts.csv")
+        assert f.shape == (len(tasks) * h, 2 + 30)
+        np.testing.assert_array_equal(f[:4, :2], [[50, 51], [50, 52], [50, 53], [51, 52]])
+        p = yio.readdlm(tmp_path / f"1C__thread_id__9__{wt}_window_fitted_params.csv")
+        assert p.shape == (len(tasks), 21)
+        np.testing.assert_array_equal(p[:, 0], tasks)
+        for what, rows in (("fl1", 30), ("fl2", 30), ("factors", 3), ("states", 1)):
+            t = yio.readdlm(tmp_path / f"1C__thread_id__9__{wt}_window_{what}.csv")
+            assert t.shape == (len(tasks) * h, 2 + rows), (wt, what, t.shape)

@@ -8,7 +8,15 @@ Rule (tests/test_gpu_parity.py): within 1e-9 of the oracle, relative to the logl
 (max(|ll|, ½·nterms·N·log 2π): short random panels can sum to ≈ 0); where the two differ by more,
 the binary128 restatement (oracle/yfm_truth.c, pinned to the 40-digit dense one) adjudicates: the
 kernel must be at least as close to it as the oracle (factor 1, every model kind, TVλ in the
-default certified precision).  −Inf / NaN patterns must match exactly."""
+default certified precision).  −Inf / NaN patterns must match exactly.  The same rule with |ll|
+alone as the denominator is gated too (round 3: 0 failures over the 62,787 finite candidates of
+3,000 cases; 148 of them are within 1e-9 of the oracle only by the term-scale denominator and are
+then closer to the truth than the oracle); YFM_SWEEP_REPORT=<file> appends one JSON line per case
+(profiles/r3/random_sweep/).
+
+The default suite runs seeds 0-11 plus every seed a 3,000-case sweep has ever failed (KNOWN_HARD:
+GNS5 with N ∈ {1, 3, 7, 12, 33, 64} and DNS with N = 1 — ill-conditioned or rank-deficient Z'Z,
+evaluated on the double-double capacitance path since round 3)."""
 from __future__ import annotations
 
 import ctypes
@@ -68,7 +76,13 @@ def random_case(rng, kind):
     return N, T, mats, Y, Th, space, T_use
 
 
-@pytest.mark.parametrize("seed", range(int(os.environ.get("YFM_RANDOM_SEEDS", "12"))))  # a wider sweep on demand
+# seeds a 3,000-case sweep failed in round 2 (profiles/r2/random_sweep/random3000_last_build.log)
+KNOWN_HARD = (244, 405, 1078, 1546, 1603, 1804, 2038, 2473, 2686)
+_N_SEEDS = int(os.environ.get("YFM_RANDOM_SEEDS", "12"))  # a wider sweep on demand
+SEEDS = sorted(set(range(_N_SEEDS)) | set(KNOWN_HARD))
+
+
+@pytest.mark.parametrize("seed", SEEDS)
 def test_random_cases_vs_c_oracle(engine, seed):
     rng = np.random.default_rng(1000 + seed)
     kind = [KIND_DNS, KIND_GNS, KIND_TVL][seed % 3]
@@ -96,10 +110,27 @@ def test_random_cases_vs_c_oracle(engine, seed):
     err = np.zeros_like(ref)
     err[fin] = np.abs(got[fin] - ref[fin]) / np.maximum(scale[fin], 1e-300)
     assert np.all((ref[fin] != 0.0) | (got[fin] == 0.0)), what  # loglik exactly 0 (T_use ≤ 2) is exact
+    # the same rule with |ll| alone as the denominator
+    err_ll = np.zeros_like(ref)
+    err_ll[fin] = np.abs(got[fin] - ref[fin]) / np.maximum(np.abs(ref[fin]), 1e-300)
+    strict_fail = [int(b) for b in np.flatnonzero(fin & (err_ll > 1e-9))
+                   if abs(got[b] - truth[b]) > abs(ref[b] - truth[b])]
+    relaxed_only = [int(b) for b in np.flatnonzero(fin & (err_ll > 1e-9) & (err <= 1e-9))]
+    rep = os.environ.get("YFM_SWEEP_REPORT")
+    if rep:
+        import json
+        with open(rep, "a") as fh:
+            fh.write(json.dumps(dict(seed=seed, kind=kind, N=N, T=T, n=int(fin.sum()), strict_fail=strict_fail,
+                                     within_only_by_term_scale=relaxed_only, deferred=engine_deferred(engine))) + "\n")
     for b in np.flatnonzero(fin & (err > 1e-9)):
         e_gt = abs(got[b] - truth[b]) / max(abs(truth[b]), scale[b])
         e_or = abs(ref[b] - truth[b]) / max(abs(truth[b]), scale[b])
         assert e_gt <= e_or, (what, b, err[b], e_gt, e_or)
+    assert not strict_fail, (what, strict_fail, got[strict_fail], ref[strict_fail], truth[strict_fail])
+
+
+def engine_deferred(engine):
+    return engine.last_deferred()
 
 
 @pytest.mark.parametrize("seed", range(6))

@@ -72,10 +72,11 @@ struct DevBuf {
 // Per-launch device work buffers.  A context owns one; the estimation driver adds one per extra
 // concurrent stream (launches in flight on different streams must not share them).
 struct yfm::Workspace {
-  DevBuf flags;       // 4 × unsigned int: n_init_throw, n_neg_inf, deferred-candidate count, pad
+  DevBuf flags;       // 4 × unsigned int: n_init_throw, n_neg_inf, deferral list length, n_deferred
   DevBuf scratch;     // per-candidate work records (TVλ / GNS5 / two-wave DNS init)
   DevBuf scratch_dd;  // TVλ double-double records (YFM_PREC_CERTIFIED)
-  DevBuf defer;       // list of candidates handed from the per-lane to the group kernel
+  DevBuf defer;       // candidates handed from the FP64 fixed-loading kernels to the dd kernel
+  DevBuf scratch_fd;  // their double-double records (yfm_fixedz_dd.hip)
 };
 
 struct yfm_ctx {
@@ -88,11 +89,12 @@ struct yfm_ctx {
   DevBuf panel, mats, raw;
   // staging for host-pointer calls
   DevBuf theta, out, tuse, rec_beta, rec_P;
-  DevBuf flags;  // 4 × unsigned int: n_init_throw, n_neg_inf, deferred-candidate count, pad
+  DevBuf flags;  // 4 × unsigned int: n_init_throw, n_neg_inf, deferral list length, n_deferred
   DevBuf scratch;  // per-candidate work records (TVλ init)
   DevBuf scratch_dd;  // TVλ double-double records (YFM_PREC_CERTIFIED)
   DevBuf traj, init_bad;       // trajectory-mode state records, per-candidate init-throw marks
-  DevBuf defer;                // list of candidates handed from the per-lane to the group kernel
+  DevBuf defer;                // candidates handed from the FP64 fixed-loading kernels to the dd kernel
+  DevBuf scratch_fd;           // their double-double records (yfm_fixedz_dd.hip)
   DevBuf tiled_raw, tiled_panel;  // get_loss_array with K > 1 passes: the panel tiled K times
   // TVλ maturity-jump tables, one per lane count L = 2^l (built lazily, reset by set_panel)
   std::vector<double> mats_host;
@@ -198,11 +200,12 @@ int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int 
   DevBuf& w_scratch = ws ? ws->scratch : ctx->scratch;
   DevBuf& w_scratch_dd = ws ? ws->scratch_dd : ctx->scratch_dd;
   DevBuf& w_defer = ws ? ws->defer : ctx->defer;
-  // one fill resets the flag counters (unless a pipelined chunk continues them) and the
-  // deferred-candidate count: flags.p = [n_init_throw, n_neg_inf, defer_count, pad]
+  DevBuf& w_scratch_fd = ws ? ws->scratch_fd : ctx->scratch_fd;
+  // one fill resets the flag counters (unless a pipelined chunk continues them) and this launch's
+  // deferral list length: flags.p = [n_init_throw, n_neg_inf, defer_count, n_deferred]
   {
     unsigned int* f = static_cast<unsigned int*>(w_flags.p);
-    YFM_HIP_CHECK(hipMemsetAsync(reset_flags ? f : f + 2, 0, (reset_flags ? 3 : 1) * sizeof(unsigned int), s));
+    YFM_HIP_CHECK(hipMemsetAsync(reset_flags ? f : f + 2, 0, (reset_flags ? 4 : 1) * sizeof(unsigned int), s));
   }
   if (B == 0) return YFM_OK;
   yfm::LaunchArgs a;
@@ -253,21 +256,22 @@ int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int 
       e = yfm::launch_tvl(a, g, lanes);
     }
   } else {
-    // N ≤ 64: one filter per lane (MFMA Z'y), then the lane-group kernel for the candidates it
-    // deferred (ill-conditioned Z'Z); larger N: one filter per lane group for every candidate
+    // N ≤ 64: one filter per lane (MFMA Z'y); larger N: one filter per lane group.  Either defers
+    // the candidates with an ill-conditioned Z'Z, which the double-double kernel then evaluates
+    YFM_HIP_CHECK(w_defer.ensure(sizeof(int) * (size_t)B));
+    YFM_HIP_CHECK(w_scratch_fd.ensure(yfm::fixedz_dd_scratch_bytes(kind, B)));
+    a.defer_count = reinterpret_cast<int*>(static_cast<unsigned int*>(w_flags.p) + 2);  // zeroed above
+    a.defer_list = static_cast<int*>(w_defer.p);
     if (yfm::fixedz_np_for(ctx->N) > 0) {
-      YFM_HIP_CHECK(w_defer.ensure(sizeof(int) * (size_t)B));
-      a.defer_count = reinterpret_cast<int*>(static_cast<unsigned int*>(w_flags.p) + 2);  // zeroed above
-      a.defer_list = static_cast<int*>(w_defer.p);
       if (const size_t sb = yfm::fixedz_scratch_bytes(kind, B)) {
         YFM_HIP_CHECK(w_scratch.ensure(sb));
         a.scratch = static_cast<double*>(w_scratch.p);
       }
       e = yfm::launch_fixedz(kind, a);
-      if (e == hipSuccess) e = yfm::launch_fixedz_group(kind, a);
     } else {
       e = yfm::launch_fixedz_group(kind, a);
     }
+    if (e == hipSuccess) e = yfm::launch_fixedz_dd(kind, a, static_cast<double*>(w_scratch_fd.p));
   }
   if (e != hipSuccess) return set_error(YFM_EHIP, "kernel launch: %s", hipGetErrorString(e));
   return YFM_OK;
@@ -387,7 +391,8 @@ void yfm_destroy(yfm_ctx* ctx) {
   for (DevBuf* b : {&ctx->panel, &ctx->mats, &ctx->raw, &ctx->theta, &ctx->out, &ctx->tuse, &ctx->rec_beta,
                     &ctx->rec_P, &ctx->flags, &ctx->scratch})
     b->release();
-  for (DevBuf* b : {&ctx->traj, &ctx->init_bad, &ctx->tiled_raw, &ctx->tiled_panel, &ctx->defer}) b->release();
+  for (DevBuf* b : {&ctx->traj, &ctx->init_bad, &ctx->tiled_raw, &ctx->tiled_panel, &ctx->defer, &ctx->scratch_fd})
+    b->release();
   ctx->scratch_dd.release();
   for (DevBuf& b : ctx->gap_buf) b.release();
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -571,6 +576,14 @@ int yfm_last_batch_flags(yfm_ctx* ctx, long long* n_init_throw, long long* n_neg
   return YFM_OK;
 }
 
+int yfm_last_batch_deferred(yfm_ctx* ctx, long long* n_deferred) {
+  if (int r = check_ctx(ctx)) return r;
+  unsigned int h[4] = {0, 0, 0, 0};
+  YFM_HIP_CHECK(hipMemcpy(h, ctx->flags.p, sizeof(h), hipMemcpyDeviceToHost));
+  if (n_deferred) *n_deferred = h[3];
+  return YFM_OK;
+}
+
 int yfm_gamma_dim(int model_kind) { return gamma_dim(model_kind); }
 
 int yfm_predict(yfm_ctx* ctx, int model_kind, int param_space, const double* theta, int P, int B, const int* T_use,
@@ -693,7 +706,7 @@ Workspace* workspace_create() {
 
 void workspace_destroy(Workspace* w) {
   if (!w) return;
-  for (DevBuf* b : {&w->flags, &w->scratch, &w->scratch_dd, &w->defer}) b->release();
+  for (DevBuf* b : {&w->flags, &w->scratch, &w->scratch_dd, &w->defer, &w->scratch_fd}) b->release();
   delete w;
 }
 

@@ -163,4 +163,142 @@ __device__ __forceinline__ dd dd_exp(dd x) {
   return dd_ldexp(e, (int)k);
 }
 
+// ---- shared by the double-double filters (yfm_tvl_dd.hip, yfm_fixedz_dd.hip) ----
+
+// −λ·m in dd for exp(−λm); a product that overflows (λ near the FP64 range) is −Inf, whose exp is
+// 0 as in the reference — TwoProd's error term would be Inf − Inf = NaN there
+__device__ __forceinline__ dd neg_rate(dd lam, double m) {
+  const dd p = dd_mul_d(lam, m);
+  return __builtin_isfinite(p.hi) ? dd_neg(p) : dd{-(lam.hi * m), 0.0};
+}
+
+// Gaussian elimination with partial pivoting (first max |hi|, the getf2 rule) on an n×n dd
+// system with R right-hand sides; false on an exact zero pivot (where getrf reports info > 0).
+template <int n, int R>
+__device__ __forceinline__ bool dd_gauss(dd (&A)[n][n], dd (&X)[n][R], dd* det_out = nullptr) {
+  bool ok = true;
+  double sgn = 1.0;
+  dd det = dd_make(1.0);
+#pragma unroll
+  for (int k = 0; k < n; ++k) {
+    int p = k;
+    double amax = fabs(A[k][k].hi);
+#pragma unroll
+    for (int i = k + 1; i < n; ++i) {
+      const double a = fabs(A[i][k].hi);
+      const bool gt = a > amax;
+      amax = gt ? a : amax;
+      p = gt ? i : p;
+    }
+    sgn = (p != k) ? -sgn : sgn;
+#pragma unroll
+    for (int i = k + 1; i < n; ++i) {
+      const bool s = (p == i);
+#pragma unroll
+      for (int c = k; c < n; ++c) {
+        const dd a = A[k][c], b = A[i][c];
+        A[k][c] = s ? b : a;
+        A[i][c] = s ? a : b;
+      }
+#pragma unroll
+      for (int c = 0; c < R; ++c) {
+        const dd a = X[k][c], b = X[i][c];
+        X[k][c] = s ? b : a;
+        X[i][c] = s ? a : b;
+      }
+    }
+    const dd piv = A[k][k];
+    ok = ok && (piv.hi != 0.0);
+    if (det_out) det = dd_mul(det, piv);
+    const dd r = dd_rcp(piv);
+#pragma unroll
+    for (int i = k + 1; i < n; ++i) {
+      const dd l = dd_mul(A[i][k], r);
+#pragma unroll
+      for (int c = k + 1; c < n; ++c) A[i][c] = dd_sub(A[i][c], dd_mul(l, A[k][c]));
+#pragma unroll
+      for (int c = 0; c < R; ++c) X[i][c] = dd_sub(X[i][c], dd_mul(l, X[k][c]));
+    }
+    A[k][k] = r;  // keep the reciprocal pivot for the back substitution
+  }
+#pragma unroll
+  for (int k = n - 1; k >= 0; --k) {
+#pragma unroll
+    for (int c = 0; c < R; ++c) {
+      dd s = X[k][c];
+#pragma unroll
+      for (int j = k + 1; j < n; ++j) s = dd_sub(s, dd_mul(A[k][j], X[j][c]));
+      X[k][c] = dd_mul(s, A[k][k]);
+    }
+  }
+  if (det_out) *det_out = sgn < 0 ? dd_neg(det) : det;
+  return ok;
+}
+
+// log of a positive dd to ~u² absolute: FP64 seed + one Newton step on e^y = x
+__device__ __forceinline__ dd dd_log(dd x) {
+  const double y0 = log(x.hi);
+  const dd e = dd_exp(dd_make(-y0));
+  const dd t = dd_add_d(dd_mul(x, e), -1.0);  // x·e^{−y0} − 1
+  return dd_add_d(t, y0);
+}
+
+// transformations.jl:21-26 as written (2y/(1+y) − 1), in dd
+__device__ __forceinline__ dd dd_from_R_to_11(double x) {
+  const dd y = dd_exp(dd_make(x));
+  if (!(y.hi < __builtin_inf())) return {__builtin_nan(""), 0.0};  // Inf/Inf
+  return dd_add_d(dd_div(dd_mul_d(y, 2.0), dd_add_d(y, 1.0)), -1.0);
+}
+
+// Sum of an unnormalised dd over the aligned group of L lanes: each butterfly level pairs
+// every lane with its partner and both form the same exact-leading-part sum, so all lanes
+// of the group end with bitwise the same value.
+template <int LVL>
+__device__ __forceinline__ void pair_exchange(double x, double& a, double& b) {
+  const int lo = __double2loint(x), hi = __double2hiint(x);
+  if constexpr (LVL <= 3) {
+    constexpr int ctrl = LVL == 0 ? 0xB1 : LVL == 1 ? 0x4E : LVL == 2 ? 0x141 : 0x140;
+    const int plo = __builtin_amdgcn_mov_dpp(lo, ctrl, 0xf, 0xf, true);
+    const int phi = __builtin_amdgcn_mov_dpp(hi, ctrl, 0xf, 0xf, true);
+    const double p = __hiloint2double(phi, plo);
+    // canonical order (lower lane's value first) so both partners compute the same bits
+    const bool lower = LVL == 0 ? !(threadIdx.x & 1) : LVL == 1 ? !(threadIdx.x & 2)
+                     : LVL == 2 ? !(threadIdx.x & 4) : !(threadIdx.x & 8);
+    a = lower ? x : p;
+    b = lower ? p : x;
+  } else if constexpr (LVL == 4) {
+    const auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    a = __hiloint2double(rh[0], rl[0]);
+    b = __hiloint2double(rh[1], rl[1]);
+  } else {
+    const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    a = __hiloint2double(rh[0], rl[0]);
+    b = __hiloint2double(rh[1], rl[1]);
+  }
+}
+
+template <int LVL>
+__device__ __forceinline__ void acc_level(double& hi, double& lo) {
+  double h0, h1, l0, l1;
+  pair_exchange<LVL>(hi, h0, h1);
+  pair_exchange<LVL>(lo, l0, l1);
+  const dd s = two_sum(h0, h1);
+  hi = s.hi;
+  lo = (l0 + l1) + s.lo;
+}
+
+template <int L>
+__device__ __forceinline__ dd group_sum_acc(dd_acc a) {
+  double hi = a.hi, lo = a.lo;
+  if constexpr (L >= 2) acc_level<0>(hi, lo);
+  if constexpr (L >= 4) acc_level<1>(hi, lo);
+  if constexpr (L >= 8) acc_level<2>(hi, lo);
+  if constexpr (L >= 16) acc_level<3>(hi, lo);
+  if constexpr (L >= 32) acc_level<4>(hi, lo);
+  if constexpr (L >= 64) acc_level<5>(hi, lo);
+  return two_sum(hi, lo);  // |lo| may exceed |hi| after cancellation
+}
+
 }  // namespace yfm

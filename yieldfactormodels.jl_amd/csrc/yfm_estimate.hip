@@ -114,6 +114,16 @@ double to_unconstrained(int code, double x) {
 }
 
 // Minimal fork-join pool for the per-round host work (chains are independent).
+//
+// Round protocol (no item can run twice or leak into the next round):
+//   run():   with no round open and no worker inside one, write the round's parameters, then
+//            open it (open_ = its generation, seq_cst); drain; wait until every item is done;
+//            close it (open_ = 0); wait until no worker is inside it (active_ == 0).
+//   worker:  active_ += 1, THEN read open_ (both seq_cst); only a worker that sees the round
+//            open touches its parameters; active_ −= 1 when it leaves.
+// A worker that registers after run() saw active_ == 0 reads open_ after that point in the
+// single total order, so it sees 0 (and leaves without reading anything) or a later round whose
+// parameters were written before that round was opened.
 class Pool {
  public:
   explicit Pool(int n) {
@@ -123,12 +133,13 @@ class Pool {
     {
       std::lock_guard<std::mutex> g(m_);
       stop_ = true;
-      stop_a_.store(true, std::memory_order_release);
+      stop_a_.store(true);
     }
     cv_.notify_all();
     for (auto& t : th_) t.join();
   }
-  // f(i) for i in [0, n), items handed out in chunks; returns when all are done
+  // f(i) for i in [0, n), items handed out in chunks; returns when all are done and every worker
+  // has left the round
   template <class F>
   void run(int n, int chunk, F&& f) {
     if (th_.empty() || n <= chunk) {
@@ -144,13 +155,15 @@ class Pool {
       chunk_ = chunk;
       next_.store(0);
       done_.store(0);
-      ++gen_;
-      gen_a_.store(gen_, std::memory_order_release);
+      gen_ = gen_ == 0x7fffffff ? 1 : gen_ + 1;
+      open_.store(gen_);
       wake = sleepers_ > 0;
     }
     if (wake) cv_.notify_all();
     drain();
-    while (done_.load(std::memory_order_acquire) < n) __builtin_ia32_pause();
+    while (done_.load() < n) __builtin_ia32_pause();
+    open_.store(0);
+    while (active_.load() != 0) __builtin_ia32_pause();
     std::lock_guard<std::mutex> g(m_);
     job_ = nullptr;
   }
@@ -162,7 +175,7 @@ class Pool {
       if (i0 >= n_) return;
       const int i1 = std::min(n_, i0 + chunk_);
       for (int i = i0; i < i1; ++i) (*job_)(i);
-      done_.fetch_add(i1 - i0, std::memory_order_release);
+      done_.fetch_add(i1 - i0);
     }
   }
   // Rounds come every few hundred µs: a worker spins for the next one (a futex wake-up costs tens
@@ -171,25 +184,30 @@ class Pool {
     int seen = 0;
     for (;;) {
       const auto t0 = std::chrono::steady_clock::now();
-      for (int k = 0; gen_a_.load(std::memory_order_acquire) == seen && !stop_a_.load(std::memory_order_acquire); ++k) {
+      for (int k = 0; (open_.load() == 0 || open_.load() == seen) && !stop_a_.load(); ++k) {
         __builtin_ia32_pause();
         if ((k & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
       }
       {
         std::unique_lock<std::mutex> lk(m_);
-        if (!stop_ && gen_ == seen) {
+        auto idle = [&] {
+          const int o = open_.load();
+          return o == 0 || o == seen;
+        };
+        if (!stop_ && idle()) {
           ++sleepers_;
-          cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+          cv_.wait(lk, [&] { return stop_ || !idle(); });
           --sleepers_;
         }
         if (stop_) return;
-        if (!job_) {  // the round this generation announced is already over
-          seen = gen_;
-          continue;
-        }
-        seen = gen_;
       }
-      drain();
+      active_.fetch_add(1);
+      const int g = open_.load();
+      if (g != 0 && g != seen) {
+        seen = g;
+        drain();
+      }
+      active_.fetch_sub(1);
     }
   }
   std::vector<std::thread> th_;
@@ -198,7 +216,7 @@ class Pool {
   std::function<void(int)>* job_ = nullptr;
   int n_ = 0, chunk_ = 1, gen_ = 0, sleepers_ = 0;
   bool stop_ = false;
-  std::atomic<int> next_{0}, done_{0}, gen_a_{0};
+  std::atomic<int> next_{0}, done_{0}, open_{0}, active_{0};
   std::atomic<bool> stop_a_{false};
 };
 

@@ -79,14 +79,22 @@ __device__ __forceinline__ void collapsed_update(const double (&zt)[M - 1], doub
 }
 
 
-// CAP: whether this filter runs the capacitance form itself.  The one-filter-per-lane kernel
-// (CAP = false) defers lanes whose Z'Z is ill-conditioned to the lane-group kernel, which has
-// the per-maturity data the capacitance form's innovation needs (CAP = true).
-template <int M, int LEAD, bool RECORD, bool CAP>
+// Lanes whose Z'Z is ill-conditioned (κ₁ ≥ kCollapsedKappa), singular, or has fewer maturities than
+// states are not evaluated here: the kernels append them to a deferral list and the double-double
+// capacitance kernel (yfm_fixedz_dd.hip) evaluates them afterwards.
+//
+// The collapsed form's rounding grows with κ(Z'Z) through R = σ²(Z'Z)⁻¹ and ĉ = (Z'Z)⁻¹Z'y
+// (measured: up to ≈ κ·3e-17 relative on the loglik, e.g. 1.8e-9 at κ₁ = 5e7 on a 40-step
+// GNS5 panel, where the reference's dense path is 1e-13 from exact).  κ₁ is ≈ 400 for DNS on the
+// usual grids and 2.5e4 … 7.0e5 over the 1,048,576 GNS5 candidates of config 5, so at 1e6 no
+// benchmark lane is deferred while the error of every collapsed lane stays ≲ 3e-11.
+constexpr double kCollapsedKappa = 1e6;
+
+template <int M, int LEAD, bool RECORD>
 struct FixedZFilter {
   Params<M, LEAD> p;
   double sigma2, rsig2;
-  double R[M][M];  // σ²(Z'Z)⁻¹ on collapsed lanes, Z'Z on capacitance lanes
+  double R[M][M];  // σ²(Z'Z)⁻¹ (meaningful on collapsed lanes only)
   double logdetG = 0.0;
   bool collapsed = false, init_ok = false;
   int N = 0;
@@ -96,17 +104,15 @@ struct FixedZFilter {
   bool neg = false;
   double last_det = 0.0, last_q = 0.0;  // fresh model: F = 0, F⁻¹ = 0, v = 0 (kalmanbasemodel.jl:65-67)
 
-  // G = Z'Z → R, log det G, collapsed vs capacitance; then initialize_filter.
+  // G = Z'Z → R, log det G, collapsed or deferred; then initialize_filter.
   // do_init = false: the caller loads the initial state itself (fixedz_init_kernel's record)
   __device__ __forceinline__ void setup(const double (&G)[M][M], int N_, bool do_init = true) {
     N = N_;
     sigma2 = p.sigma2;
     rsig2 = 1.0 / sigma2;
     double A[M][M], X[M][M];
-    double hadamard = 1.0;
 #pragma unroll
     for (int i = 0; i < M; ++i) {
-      hadamard *= G[i][i];
 #pragma unroll
       for (int j = 0; j < M; ++j) {
         A[i][j] = G[i][j];
@@ -118,11 +124,7 @@ struct FixedZFilter {
 #pragma unroll
     for (int i = 0; i < M; ++i) detG *= A[i][i];
     detG = fabs(detG);
-    // The collapsed form's rounding grows with κ(Z'Z) (measured: ≈ κ·3e-18 relative on the
-    // loglik); κ₁ = ‖G‖₁‖G⁻¹‖₁ is ≈ 400 for DNS and ≤ 3e5 for GNS5 on the usual maturity grids,
-    // ~1e15 when the loadings are collinear (e.g. three long maturities).  Above 1e8 the lane
-    // takes the capacitance form, which does not invert Z'Z.
-    double nG = 0.0, nX = 0.0;
+    double nG = 0.0, nX = 0.0;  // κ₁ = ‖G‖₁‖G⁻¹‖₁
 #pragma unroll
     for (int j = 0; j < M; ++j) {
       double cg = 0.0, cx = 0.0;
@@ -134,24 +136,19 @@ struct FixedZFilter {
       nG = fmax(nG, cg);
       nX = fmax(nX, cx);
     }
-    (void)hadamard;
-    collapsed = ok && (N >= M) && (nG * nX < 1e8);
+    collapsed = ok && (N >= M) && (nG * nX < kCollapsedKappa);
     logdetG = collapsed ? log(detG) : 0.0;
 #pragma unroll
     for (int i = 0; i < M; ++i)
 #pragma unroll
-      for (int j = 0; j < M; ++j) R[i][j] = collapsed ? sigma2 * 0.5 * (X[i][j] + X[j][i]) : G[i][j];
+      for (int j = 0; j < M; ++j) R[i][j] = sigma2 * 0.5 * (X[i][j] + X[j][i]);
     if (do_init) init_ok = init_state<M, LEAD>(p, beta, Pm);
   }
 
   // One filter! call on column t given z̃_t (zc), (ȳ, ỹ'ỹ) = yb and (nan flag, y'y) = meta.
-  // `fast`: the caller guarantees t ≥ 1, a data column, an active collapsed lane (no masking).
-  // `resid(beta, u, vv)`: u = Z'v and v'v of the innovation v = y_t − Zβ formed per maturity,
-  // as the reference does (filter.jl:143-144) — used on capacitance lanes (Z'Z near-singular),
-  // where reconstructing v'v from y'y, Z'y and Z'Z would lose ‖Z‖‖β‖/‖v‖ digits.
-  template <class Resid>
+  // `fast`: the caller guarantees t ≥ 1, a data column and an active lane (no masking).
   __device__ __forceinline__ void step(int t, const double (&zc)[M - 1], double2 yb_c, double2 meta_c, bool fast,
-                                       int my_steps, int my_data, Resid&& resid) {
+                                       int my_steps, int my_data) {
     if (fast) {
       double bf[M], Pf[M][M], det, q;
       collapsed_update<M>(zc, yb_c.x, yb_c.y, R, rsig2, beta, Pm, bf, Pf, det, q);
@@ -189,33 +186,7 @@ struct FixedZFilter {
     double det, q;
     double bf[M];
     double Pf[M][M];
-    if (!CAP || collapsed) {
-      collapsed_update<M>(zc, yb_c.x, yb_c.y, R, rsig2, beta, Pm, bf, Pf, det, q);
-    } else if constexpr (CAP) {
-      // capacitance form (R holds G = Z'Z on these lanes)
-      double u[M], vv;
-      resid(beta, u, vv);
-      double W[M][M];
-      Capacitance<M, true>::solve(Pm, R, sigma2, W, det);
-#pragma unroll
-      for (int i = 0; i < M; ++i)
-#pragma unroll
-        for (int j = 0; j < i; ++j) W[i][j] = W[j][i];
-      double uk = 0.0;
-#pragma unroll
-      for (int i = 0; i < M; ++i) {
-        double s = 0.0;
-#pragma unroll
-        for (int j = 0; j < M; ++j) s = fma(W[i][j], u[j], s);
-        bf[i] = beta[i] + s;
-        uk = fma(u[i], s, uk);
-      }
-      q = (vv - uk) * rsig2;
-#pragma unroll
-      for (int i = 0; i < M; ++i)
-#pragma unroll
-        for (int j = i; j < M; ++j) Pf[i][j] = sigma2 * W[i][j];
-    }
+    collapsed_update<M>(zc, yb_c.x, yb_c.y, R, rsig2, beta, Pm, bf, Pf, det, q);
     const bool upd = det != 0.0;  // inv(F) threw: return without the update (filter.jl:151-154)
     if (upd) propagate_state<M, LEAD>(p, bf, Pf, beta, Pm);
     last_det = det;

@@ -10,6 +10,8 @@
 // column and the group reduces them with DPP / permlane butterflies (group_sum, no LDS).
 // Z'Z is formed the same way once.  Every lane of the group then runs the M×M update
 // redundantly, so the state stays replicated and no broadcast is needed; lane 0 writes.
+// Candidates with an ill-conditioned Z'Z are appended to the deferral list (as in the per-lane
+// kernel) for the double-double capacitance kernel (yfm_fixedz_dd.hip).
 //
 // Panel: the prepared centered panel (prep_panel_kernel layout, ldp doubles per column),
 // TC columns per LDS chunk, the next chunk prefetched into registers (as yfm_tvl.hip).
@@ -35,7 +37,7 @@ __global__ __launch_bounds__(kGBlock, 2) void fixedz_group_kernel(
     const double* __restrict__ theta, int P, int B, int space, const double* __restrict__ panel, int ldp, int np,
     int T, int N, int TC, const double* __restrict__ mats, const int* __restrict__ T_use, double* __restrict__ out,
     unsigned int* __restrict__ flags, double* __restrict__ rec_beta, double* __restrict__ rec_P, int horizon,
-    int rec_len, const int* __restrict__ defer_list, const int* __restrict__ defer_count) {
+    int rec_len, int* __restrict__ defer_list, int* __restrict__ defer_count) {
   constexpr int NZ = M - 1;
   constexpr int GPB = kGBlock / L;  // filters per block
   constexpr int MPL = group_max_per_lane<M>();
@@ -46,17 +48,9 @@ __global__ __launch_bounds__(kGBlock, 2) void fixedz_group_kernel(
 
   const int tid = threadIdx.x;
   const int j = tid % L;
-  // deferred mode: filter g evaluates candidate defer_list[g] (ill-conditioned Z'Z lanes of
-  // the per-lane kernel), g < *defer_count; blocks past the list exit before any barrier
-  const int g = blockIdx.x * GPB + tid / L;
-  int nd = B;
-  if (defer_list) {
-    nd = *defer_count;
-    if ((int)blockIdx.x * GPB >= nd) return;
-  }
-  const bool live = g < nd;
-  const int b = defer_list ? (live ? defer_list[g] : 0) : g;
-  const int bb = live ? b : (defer_list ? defer_list[0] : B - 1);
+  const int b = blockIdx.x * GPB + tid / L;
+  const bool live = b < B;
+  const int bb = live ? b : B - 1;
   const int nobs = T_use ? T_use[bb] : T;
   const int my_steps = horizon > 0 ? nobs + horizon : nobs - 1;  // as yfm_kernels.hip
   const int my_data = horizon > 0 ? nobs : nobs - 1;
@@ -65,7 +59,7 @@ __global__ __launch_bounds__(kGBlock, 2) void fixedz_group_kernel(
   __syncthreads();
   atomicMax(&s_nobs_max, live ? my_steps : 0);
 
-  FixedZFilter<M, LEAD, RECORD, true> f;
+  FixedZFilter<M, LEAD, RECORD> f;
   decode_params<M, LEAD>(theta + (size_t)bb * P, space, f.p);
 
   // this lane's loadings (dns.jl:51-65; the GNS5 extension adds a second (S, C) pair)
@@ -109,6 +103,8 @@ __global__ __launch_bounds__(kGBlock, 2) void fixedz_group_kernel(
     }
   }
   f.setup(G, N);
+  const bool defer = live && !f.collapsed;
+  if (defer && j == 0) defer_list[atomicAdd(defer_count, 1)] = b;
 
   __syncthreads();
   const int nsteps = max(s_nobs_max, 0);
@@ -157,34 +153,9 @@ __global__ __launch_bounds__(kGBlock, 2) void fixedz_group_kernel(
     for (int c = 0; c < NZ; ++c) zc[c] = group_sum<L>(zc[c]);
     const double2 yb = *reinterpret_cast<const double2*>(col + np);
     const double2 meta = *reinterpret_cast<const double2*>(col + np + 2);
-    // capacitance lanes (near-singular Z'Z): the innovation per owned maturity, group-reduced
-    auto resid = [&](const double (&bt)[M], double (&u)[M], double& vv) {
-      double acc[M + 1];
-#pragma unroll
-      for (int c = 0; c <= M; ++c) acc[c] = 0.0;
-#pragma unroll
-      for (int k = 0; k < MPL; ++k) {
-        const int i = j + k * L;
-        if (i < N) {
-          double yh = bt[0];
-#pragma unroll
-          for (int c = 0; c < NZ; ++c) yh = fma(Zl[k][c], bt[c + 1], yh);
-          const double v = (col[i] + yb.x) - yh;
-          acc[0] += v;
-#pragma unroll
-          for (int c = 0; c < NZ; ++c) acc[c + 1] = fma(Zl[k][c], v, acc[c + 1]);
-          acc[M] = fma(v, v, acc[M]);
-        }
-      }
-#pragma unroll
-      for (int c = 0; c <= M; ++c) acc[c] = group_sum<L>(acc[c]);
-#pragma unroll
-      for (int c = 0; c < M; ++c) u[c] = acc[c];
-      vv = acc[M];
-    };
-    f.step(t, zc, yb, meta, false, my_steps, my_data, resid);
+    f.step(t, zc, yb, meta, false, my_steps, my_data);
     if constexpr (RECORD) {
-      if (live && j == 0) f.record(t, b, my_steps, rec_len, rec_beta, rec_P);
+      if (live && !defer && j == 0) f.record(t, b, my_steps, rec_len, rec_beta, rec_P);
     }
     if (tt == TC - 1) {  // chunk done: its buffer takes the prefetched chunk, prefetch the one after
       __syncthreads();
@@ -194,7 +165,7 @@ __global__ __launch_bounds__(kGBlock, 2) void fixedz_group_kernel(
     }
   }
 
-  if (!live || j != 0) return;
+  if (!live || defer || j != 0) return;
   out[b] = f.loglik(nobs, flags);
 }
 
@@ -241,7 +212,7 @@ int group_lanes_for(int kind, int N) {
 }
 
 hipError_t launch_fixedz_group(int kind, const LaunchArgs& a) {
-  // a.defer_list != nullptr: evaluate only the candidates the per-lane kernel deferred
+  if (!a.defer_list || !a.defer_count) return hipErrorInvalidValue;
   const int L = group_lanes_for(kind, a.N);
   if (L < 0) return hipErrorInvalidValue;
   int TC = (kGPre * kGBlock) / a.ldp;  // columns per chunk: the prefetch registers hold ≤ kGPre·256

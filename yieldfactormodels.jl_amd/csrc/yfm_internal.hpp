@@ -21,8 +21,8 @@ struct LaunchArgs {
   double* scratch;      // per-candidate work records (tvl_scratch_bytes, fixedz_scratch_bytes)
   int horizon = 0;      // 0: loglik mode; ≥ 1: trajectory mode (predict / forecast / loss array)
   int rec_len = 0;      // recorded steps per candidate (the last rec_len), stride of rec_beta / rec_P
-  int* defer_list = nullptr;   // per-lane fixed-loading kernel → lane-group kernel hand-off (B ints)
-  int* defer_count = nullptr;  // 1 int, zeroed before the per-lane kernel
+  int* defer_list = nullptr;   // fixed-loading FP64 kernels → double-double kernel hand-off (B ints)
+  int* defer_count = nullptr;  // 1 int, zeroed before the FP64 kernel
   hipStream_t stream;
 };
 
@@ -35,6 +35,10 @@ size_t fixedz_scratch_bytes(int kind, int B);
 int group_max_n(int kind);
 int group_lanes_for(int kind, int N);
 hipError_t launch_fixedz_group(int kind, const LaunchArgs& a);
+// the deferred fixed-loading candidates (ill-conditioned Z'Z) in double-double arithmetic
+// (yfm_fixedz_dd.hip): per-candidate dd records of fixedz_dd_scratch_bytes(kind, B) bytes
+size_t fixedz_dd_scratch_bytes(int kind, int B);
+hipError_t launch_fixedz_dd(int kind, const LaunchArgs& a, double* rec);
 // TVλ EKF kernel (yfm_tvl.hip): lanes per filter for a batch, largest N, launcher
 int tvl_lanes_for(int B, int N);
 int tvl_max_n();

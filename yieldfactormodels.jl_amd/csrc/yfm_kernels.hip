@@ -19,8 +19,9 @@
 // all exact rewrites of filter.jl:143-176 (F = ZPZ' + σ²I, K = PZ'F⁻¹, I − KZ).
 // r'r is formed from CENTERED columns ỹ = y − ȳ1 (1 = Z e₁ for every candidate),
 // which removes the y'y − ŷ'ŷ cancellation.  S is factorised by LDLᵀ.
-// Lanes whose Z'Z is numerically singular (N < M, or λ so large that Z's columns
-// collapse) take the CAPACITANCE form instead: B̃ = σ²I + PG, pivoted LU,
+// Lanes whose Z'Z is ill-conditioned (κ₁ ≥ 1e6), singular, or has fewer maturities than
+// states (N < M) are appended to a deferral list and evaluated afterwards by the
+// double-double CAPACITANCE kernel (yfm_fixedz_dd.hip): B̃ = σ²I + PG, pivoted LU,
 // W = B̃⁻¹P, v'F⁻¹v = (v'v − u'Wu)/σ², P_{t|t} = σ²W, log det F = (N−M) log σ² +
 // log det B̃.
 //
@@ -266,7 +267,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     }
   }
 
-  FixedZFilter<M, LEAD, RECORD, false> f;
+  FixedZFilter<M, LEAD, RECORD> f;
   f.p = p;
   f.setup(G, N, !SPLIT_INIT);
   if constexpr (SPLIT_INIT) {
@@ -283,8 +284,8 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
       }
     f.init_ok = init_rec[(size_t)q * B + bb] != 0.0;
   }
-  // ill-conditioned Z'Z: this candidate is evaluated by the lane-group kernel instead (capacitance
-  // form with the innovation formed per maturity); its lane here runs along without writing
+  // ill-conditioned Z'Z: this candidate is evaluated by the double-double capacitance kernel
+  // instead (yfm_fixedz_dd.hip); its lane here runs along without writing
   const bool defer = live && !f.collapsed;
   if (defer) defer_list[atomicAdd(defer_count, 1)] = b;
 
@@ -330,7 +331,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   // one filter step given z̃_t (zc), (ȳ, ỹ'ỹ) and (nanflag, y'y) of column t
   auto do_step = [&](int t, const double (&zc)[NZ], double2 yb_c, double2 meta_c) {
     const bool fast = (t >= 1) && (meta_c.x == 0.0) && (t < wave_min_data) && wave_all_collapsed;
-    f.step(t, zc, yb_c, meta_c, fast, my_steps, my_data, [](const double (&)[M], double (&)[M], double&) {});
+    f.step(t, zc, yb_c, meta_c, fast, my_steps, my_data);
   };
   auto record = [&](int t) {
     if constexpr (RECORD) {

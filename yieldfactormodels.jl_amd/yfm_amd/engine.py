@@ -195,6 +195,13 @@ class Engine:
         _lib.check(self.lib.yfm_last_batch_flags(self.ctx, ctypes.byref(a), ctypes.byref(b)))
         return a.value, b.value
 
+    def last_deferred(self) -> int:
+        """Candidates of the last batch evaluated on the double-double capacitance path (fixed-loading
+        models with an ill-conditioned Z'Z; include/yfm.h yfm_last_batch_deferred)."""
+        n = ctypes.c_longlong(0)
+        _lib.check(self.lib.yfm_last_batch_deferred(self.ctx, ctypes.byref(n)))
+        return n.value
+
 
 _engines: dict[int, Engine] = {}
 _lock = threading.Lock()
