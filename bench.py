@@ -153,6 +153,38 @@ def _host_cpu() -> str:
     return "unknown"
 
 
+def cpu_topology() -> dict:
+    """The host CPU share this process may use: logical CPUs in its affinity mask, the cgroup CPU quota
+    (cpu.max; the GPU boxes grant each job a share of a larger machine), and the host's physical
+    cores.  The CPU baselines run min(affinity, quota) OpenMP threads — every CPU the job may use,
+    no more (more threads than the quota would only time-slice)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(p)
+    except (OSError, ValueError):
+        pass
+    phys = set()
+    try:
+        pid = cid = None
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("physical id"):
+                pid = line.split(":")[1].strip()
+            elif line.startswith("core id"):
+                cid = line.split(":")[1].strip()
+            elif not line.strip():
+                if cid is not None:
+                    phys.add((pid, cid))
+                pid = cid = None
+    except OSError:
+        pass
+    threads = aff if quota is None else max(1, min(aff, int(quota)))
+    return {"threads_used": threads, "affinity_cpus": aff, "cgroup_quota_cpus": quota,
+            "host_logical_cpus": os.cpu_count(), "host_physical_cores": len(phys) or None, "host_cpu": _host_cpu()}
+
+
 def _native_libs():
     """The dense port and the optimised variant built with -march=native for THIS host (the in-tree
     builds target x86-64-v3 so they load anywhere); falls back to the in-tree builds."""
@@ -203,7 +235,8 @@ def cpu_baseline(w: Workload, seconds: float, gpu_out: np.ndarray):
                                truth (oracle/yfm_truth.c): (within 1e-9, adjudicated, failing)."""
     from oracle.truth import loglik_truth
     dense, fast, flags = _native_libs()
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
+    topo = cpu_topology()
+    threads = topo["threads_used"]
     B = w.Theta.shape[1]
     # sample order: the batch as laid out, except for windows (config 4), where a seeded permutation
     # keeps the sample's mix of window lengths equal to the workload's
@@ -213,6 +246,7 @@ def cpu_baseline(w: Workload, seconds: float, gpu_out: np.ndarray):
     N, T = w.Y.shape
     win = "" if w.T_use is None else " with the workload's window lengths"
     out = {"value": rate, "unit": "evals/s", "cores": threads, "kind": "port", "host_cpu": _host_cpu(),
+           "topology": topo,
            "sample": f"{done} of the benchmark's θ (T={T}, N={N}){win}, dense N×N getrf+getri + logdet LU per step "
                      f"(oracle/yfm_oracle.c, {flags}, OpenMP {threads} threads)"}
     # a threads×64 batch at 1 thread (bounded: TVλ evals take seconds each)
@@ -227,8 +261,12 @@ def cpu_baseline(w: Workload, seconds: float, gpu_out: np.ndarray):
     ro, no, _ = _timed(fast.yfm_cpu_fast_loglik, w, order, 64 * threads if not tvl else 4 * threads, threads,
                        min(seconds, 5.0), min_chunks=2)
     ro1, no1, _ = _timed(fast.yfm_cpu_fast_loglik, w, order, 64 if not tvl else 4, 1, min(seconds, 3.0), min_chunks=2)
+    full = topo["host_physical_cores"]
     out["optimised"] = {"evals_per_s": ro, "evals_timed": no, "cores": threads, "evals_per_s_1_thread": ro1,
                         "evals_timed_1_thread": no1,
+                        "extrapolated_all_physical_cores": (ro1 * full if full else None),
+                        "extrapolation": f"1-thread rate × {full} physical cores of the host (linear scaling "
+                                         "assumed, an upper bound; only the measured rates are timed)",
                         "kind": "optimised CPU variant, NOT the reference algorithm: "
                                 + ("capacitance form, one candidate per thread" if tvl else
                                    "collapsed form of DESIGN.md §3.1, 8 candidates per SIMD vector")
@@ -376,6 +414,8 @@ def main():
     outs = [d_out, torch.empty_like(d_out)] if world > 1 else [d_out]
     k_done = [torch.cuda.Event() for _ in outs]
     c_done = [torch.cuda.Event() for _ in outs]
+    # the per-step collectives with every buffer allocated here, once (no per-step torch.full/cat)
+    reducer = D.StepReducer(counts, dev) if world > 1 else None
     k_times = []  # (start, end) HIP events around each timed launch, on the launch stream
     timing = [False]
     it = [0]
@@ -399,8 +439,8 @@ def main():
             k_done[i].record(comp)
             stream.wait_event(k_done[i])
             if w.gather:
-                D.gather_logliks(o, counts)
-            best[0] = D.best_candidate_device(o, offset)
+                reducer.gather(o)
+            best[0] = reducer.best(o, offset)
             c_done[i].record(stream)
 
     def timed(steps, warmup):
@@ -438,6 +478,7 @@ def main():
     roof = roofline(kind, args.precision, N, M, T, w.T_use, B, P, kernel_ms)
     out_host = d_out.cpu().numpy()
     n_neginf, n_nan = int(np.isneginf(out_host).sum()), int(np.isnan(out_host).sum())
+    n_deferred = eng.last_deferred()  # candidates of the last timed batch on the double-double path
 
     # TVλ: the FP64 mode of the same workload beside the certified default (not the metric's value)
     fp64_mode = None
@@ -482,6 +523,11 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(w, args.cpu_seconds, out_host)
+        cpu["gpu_over_cpu"] = {"dense_port": value / cpu["value"],
+                               "optimised": value / cpu["optimised"]["evals_per_s"],
+                               "optimised_extrapolated_all_physical_cores":
+                                   (value / cpu["optimised"]["extrapolated_all_physical_cores"]
+                                    if cpu["optimised"]["extrapolated_all_physical_cores"] else None)}
 
     if rank == 0:
         line = {
@@ -507,7 +553,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "host_pointer_rate": host_rate,
-            "outputs": {"neg_inf": n_neginf, "nan": n_nan},
+            "outputs": {"neg_inf": n_neginf, "nan": n_nan, "deferred_double_double": n_deferred},
         }
         if fp64_mode:
             line["fp64_mode"] = fp64_mode

@@ -28,7 +28,17 @@ def _lib(name: str):
 
 
 def _threads(n):
-    return n if n else int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
+    """n, else every CPU this process may use: its affinity mask, capped by the cgroup CPU quota."""
+    if n:
+        return n
+    aff = len(os.sched_getaffinity(0))
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, min(aff, int(float(q) / float(p))))
+    except (OSError, ValueError):
+        pass
+    return aff
 
 
 def _batched(fn, kind, Y, mats, Theta, space, T_use, nthreads):

@@ -84,10 +84,13 @@ def _argmax_worker(rank, world, port, ret):
     dev = D.best_candidate_device(local, offset)
     host = D.best_candidate(local, offset)
     allv = D.gather_logliks(local, [3, 2])
+    red = D.StepReducer([3, 2], local.device)  # bench.py's preallocated per-step form
+    steps = [(red.gather(local).clone(), red.best(local, offset).clone()) for _ in range(3)]
     if rank == 0:
         ret["dev"] = dev.tolist()
         ret["host"] = host
         ret["all"] = allv.tolist()
+        ret["red"] = [(g.tolist(), b.tolist()) for g, b in steps]
     dist.barrier()
     dist.destroy_process_group()
 
@@ -101,6 +104,8 @@ def test_argmax_reduce_ties_nan_and_ragged_gather():
     mp.spawn(_argmax_worker, args=(2, _free_port(), ret), nprocs=2, join=True)
     assert ret["dev"] == [5.0, 2.0] and ret["host"] == (2, 5.0)
     assert np.array_equal(np.array(ret["all"]), np.array([1.0, np.nan, 5.0, 5.0, 2.0]), equal_nan=True)
+    for g, b in ret["red"]:  # StepReducer: the same results on every step from its persistent buffers
+        assert np.array_equal(np.array(g), np.array(ret["all"]), equal_nan=True) and b == [5.0, 2.0]
 
 
 @pytest.mark.parametrize("config", [4, 5])

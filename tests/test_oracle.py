@@ -269,3 +269,26 @@ def test_edge_fixtures_reproduce():
             Yb = c["Y"] if tu is None else c["Y"][:, :tu[b]]
             ll = O.loglik(kind, c["maturities"], state_dim(kind), Yb, c["Theta"][:, b], space=space)
             assert ll == c["loglik_oracle"][b] or (np.isnan(ll) and np.isnan(c["loglik_oracle"][b]))
+
+
+@pytest.mark.parametrize("name", ["dns_c2", "gns5_c5", "tvl_c3"])
+def test_states_fixtures_reproduce(name):
+    """tests/golden/states (generator make_states_golden.py): the stored binary128 logliks are what
+    the truth library computes on the regenerated panel, the first candidate's truth trajectory is
+    reproduced bit for bit, and the dense FP64 oracle's trajectories are close to it (≤ 1e-7
+    per-step normwise — the reference's own FP64 distance from exact arithmetic at these shapes)."""
+    from oracle.truth import loglik_truth, states_truth
+    with np.load(ROOT / "tests" / "golden" / "states" / f"{name}.npz", allow_pickle=False) as z:
+        g = {k: z[k] for k in z.files}
+    kind = int(g["kind"])
+    mats = S.maturities_360() if kind == KIND_TVL else S.maturities_30()
+    Y = S.simulate_panel(kind, int(g["T"]), maturities=mats) if kind == KIND_TVL else S.simulate_panel(kind, int(g["T"]))
+    np.testing.assert_array_equal(loglik_truth(kind, Y, mats, g["Theta"]), g["ll_truth"])
+    _, beta, P = states_truth(kind, Y, mats, g["Theta"][:, 0])
+    np.testing.assert_array_equal(beta, g["beta_truth"][..., 0])
+    iu = np.triu_indices(state_dim(kind))
+    np.testing.assert_array_equal(P[iu[0], iu[1]], g["Pu_truth"][..., 0])
+    for key in ("beta", "Pu", "A"):
+        tru, ora = g[f"{key}_truth"], g[f"{key}_oracle"]
+        e = (np.abs(ora - tru).max(axis=0) / np.abs(tru).max(axis=0)).max()
+        assert e <= 1e-7, (key, e)

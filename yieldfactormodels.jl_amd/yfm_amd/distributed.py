@@ -105,6 +105,82 @@ def best_candidate_device(local: torch.Tensor, global_offset: int, group=None) -
     return allp[r].to(local.device)
 
 
+class StepReducer:
+    """The per-step collectives of a timed loop (bench.py, N > 1) with every buffer allocated once:
+    the all-gather of this rank's logliks (ragged `counts` allowed) and the argmax reduction of
+    `best_candidate_device`, both on the current stream, with no per-step tensor allocation
+    (`gather_logliks` / `best_candidate_device` allocate and concatenate on every call).
+
+    gather(local) returns the global loglik vector (a view into a persistent buffer, overwritten by
+    the next call); best(local, global_offset) returns the device tensor [best loglik, global index]
+    (also persistent)."""
+
+    def __init__(self, counts: list[int], device: torch.device, dtype=torch.float64, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.counts = [int(c) for c in counts]
+        self.m = max(self.counts) if self.counts else 0
+        cdev = _comm_device(group, device)
+        self.cdev, self.device = cdev, device
+        self.equal = all(c == self.m for c in self.counts)
+        n_local = self.counts[self.rank]
+        # send buffer: only for ragged counts (the pad tail stays NaN) or a host-staged backend
+        self.send = None
+        if not self.equal or cdev != device:
+            self.send = torch.full((self.m,), float("nan"), dtype=dtype, device=cdev)
+        self.recv = torch.empty(self.world * self.m, dtype=dtype, device=cdev)
+        self.glob = self.recv if self.equal and cdev == device else torch.empty(sum(self.counts), dtype=dtype,
+                                                                              device=device)
+        self._slices = []
+        off = 0
+        for r, c in enumerate(self.counts):
+            self._slices.append((self.recv[r * self.m: r * self.m + c], self.glob[off: off + c]))
+            off += c
+        self.n_local = n_local
+        # argmax buffers
+        self.v = torch.empty(max(n_local, 1), dtype=dtype, device=device)
+        self.vmax = torch.empty((), dtype=dtype, device=device)
+        self.imax = torch.empty((), dtype=torch.int64, device=device)
+        self.pair = torch.empty(2, dtype=dtype, device=device)
+        self.pair_c = self.pair if cdev == device else torch.empty(2, dtype=dtype, device=cdev)
+        self.allp = torch.empty(2 * self.world, dtype=dtype, device=cdev)
+        self.rmax = torch.empty((), dtype=dtype, device=cdev)
+        self.rarg = torch.empty((), dtype=torch.int64, device=cdev)
+        self.sel = torch.empty((1, 2), dtype=dtype, device=cdev)
+        self.out = torch.empty(2, dtype=dtype, device=device)
+
+    def gather(self, local: torch.Tensor) -> torch.Tensor:
+        src = local
+        if self.send is not None:
+            self.send[: self.n_local].copy_(local)
+            src = self.send
+        dist.all_gather_into_tensor(self.recv, src, group=self.group)
+        if self.glob is not self.recv:
+            for a, b in self._slices:
+                b.copy_(a)
+        return self.glob
+
+    def best(self, local: torch.Tensor, global_offset: int) -> torch.Tensor:
+        if self.n_local:
+            torch.nan_to_num(local, nan=-float("inf"), out=self.v)
+            torch.max(self.v, 0, out=(self.vmax, self.imax))
+            self.pair[0].copy_(self.vmax)
+            self.pair[1].copy_(self.imax)
+            self.pair[1].add_(float(global_offset))
+        else:  # an empty shard (B < world size) still takes part in the all-gather
+            self.pair[0].fill_(-float("inf"))
+            self.pair[1].fill_(float("inf"))
+        if self.pair_c is not self.pair:
+            self.pair_c.copy_(self.pair)
+        dist.all_gather_into_tensor(self.allp, self.pair_c, group=self.group)
+        ap = self.allp.view(self.world, 2)
+        torch.max(ap[:, 0], 0, out=(self.rmax, self.rarg))  # first maximal rank (lowest global index)
+        torch.index_select(ap, 0, self.rarg.view(1), out=self.sel)
+        self.out.copy_(self.sel.view(2))
+        return self.out
+
+
 def sharded_loglik(Theta: np.ndarray, evaluate: Callable[[np.ndarray], torch.Tensor], group=None,
                    device=None) -> GatherResult:
     """Evaluate Θ (P×B, identical on every rank) sharded over the group: rank r evaluates its
