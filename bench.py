@@ -366,6 +366,8 @@ def main():
     ap.add_argument("--precision", choices=["certified", "fp64"], default="certified",
                     help="TVλ arithmetic (include/yfm.h yfm_set_precision; the library default is certified)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--settle-seconds", type=float, default=0.5,
+                    help="untimed load before the warmup steps so the timed steps run at the card's steady clock")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-rate", action="store_true",
                     help="skip the host-pointer (PCIe-inclusive) timing, e.g. for PMC passes: its chunked "
@@ -443,11 +445,35 @@ def main():
             best[0] = reducer.best(o, offset)
             c_done[i].record(stream)
 
+    settle = {"seconds": 0.0, "steps": 0}
+
+    def settle_clock(seconds):
+        """Untimed steps until `seconds` of wall time have passed (before the W warmup steps): the card
+        leaves its idle clock only after ~0.1-0.3 s of load, so a short run timed from a cold start
+        measures the clock ramp (round 2: 20 steps gave 0.415 ms/step, 200 steps 0.364 ms)."""
+        t0 = time.perf_counter()
+        for _ in range(4):
+            step()
+        torch.cuda.synchronize(dev)
+        dt = (time.perf_counter() - t0) / 4
+        if world > 1:  # every rank runs the same number of steps (each one takes part in the collectives)
+            t = torch.tensor([dt], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        n = min(int(seconds / max(dt, 1e-6)), 20000)
+        for _ in range(n):
+            step()
+        torch.cuda.synchronize(dev)
+        settle["seconds"] += time.perf_counter() - t0
+        settle["steps"] += n + 4
+
     def timed(steps, warmup):
         """warmup untimed steps, then `steps` timed ones between barriers; (wall s, mean kernel ms)."""
         k_times.clear()
         for e in c_done:
             e.record(stream)
+        if args.settle_seconds > 0:
+            settle_clock(args.settle_seconds)
         for _ in range(warmup):
             step()
         if world > 1:
@@ -537,6 +563,8 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "clock_settle": {"seconds": round(settle["seconds"], 3), "steps": settle["steps"],
+                             "note": "untimed steps before the warmup (--settle-seconds)"},
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
             "scaling": w.scaling,

@@ -60,14 +60,19 @@ enum yfm_status {
   YFM_EUNSUPPORTED = -4 /* valid request this build has no kernel for */
 };
 
-/* precision — the arithmetic of the TVλ EKF (the fixed-loading models always run FP64: their
- * filter contracts, and the collapsed form stays within 1e-12 of exact arithmetic)
+/* precision — the arithmetic of the TVλ EKF (the fixed-loading models always run their FP64
+ * collapsed form, whose filter contracts, with ill-conditioned-loading candidates evaluated in
+ * double-double — see yfm_last_batch_deferred)
  *   YFM_PREC_CERTIFIED (default)  TVλ in double-double (~106-bit) arithmetic.  A share of TVλ
  *       candidates amplify any FP64 rounding by 1e10..1e13 over T = 600 steps, so no FP64
  *       evaluation — the reference's own dense path included — is then within 1e-9 of the
  *       exact value of filter.jl:12-80; this mode returns that value to the last FP64 bit
- *       (checked against a binary128 restatement).  ≈7× the cost of FP64.
- *   YFM_PREC_FP64  FP64 throughout: the reference's arithmetic class and the fastest path. */
+ *       (checked against a binary128 restatement).  ≈5.6× the cost of FP64.
+ *   YFM_PREC_FP64  FP64 throughout, the fastest path — an UNVERIFIED mode, not a parity mode: on
+ *       the rounding-amplifying candidates its result is as far from the exact value as FP64
+ *       arithmetic leaves it, which can be further than the reference's own dense FP64 path
+ *       (config-3 sample: up to 1.0e-2 relative from the exact value where the reference's path
+ *       is at most 7.3e-4).  Use it for screening; use YFM_PREC_CERTIFIED for results. */
 enum yfm_precision { YFM_PREC_CERTIFIED = 0, YFM_PREC_FP64 = 1 };
 
 /* Library/ABI introspection. */

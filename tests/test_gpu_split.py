@@ -1,0 +1,59 @@
+"""The two-wave DNS kernel (yfm_split.hip: a covariance wave and a mean wave per 64 candidates; opt-in
+with YFM_DNS_SPLIT=1 — measured slower) against the default one-filter-per-lane
+kernel: the same per-value arithmetic, so the same bits —
+logliks, flags, deferral, filtered states, predict and get_loss_array — on the config-2 batch, ragged
+windows with NaN columns, and every panel width the split kernel is built for (N ≤ 32)."""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+from yfm_amd import KIND_DNS
+from yfm_amd import synthetic as S
+
+pytestmark = pytest.mark.gpu
+
+
+def both(fn):
+    """(one filter per lane, two-wave split) results of fn()."""
+    a = fn()
+    os.environ["YFM_DNS_SPLIT"] = "1"
+    try:
+        b = fn()
+    finally:
+        os.environ.pop("YFM_DNS_SPLIT", None)
+    return a, b
+
+
+def test_split_bitwise_config2(engine):
+    Y = S.simulate_panel(KIND_DNS, 600)
+    engine.set_panel(Y, S.maturities_30())
+    Th = S.theta_batch(KIND_DNS, 65536)
+    a, b = both(lambda: (engine.loglik(KIND_DNS, Th), engine.last_flags(), engine.last_deferred()))
+    np.testing.assert_array_equal(a[0], b[0])
+    assert a[1] == b[1] and a[2] == b[2]
+
+
+@pytest.mark.parametrize("N", [1, 5, 8, 13, 16, 24, 30, 32])
+def test_split_bitwise_windows_nan(engine, N):
+    rng = np.random.default_rng(N)
+    mats = np.sort(rng.choice(np.arange(1, 361), N, replace=False)).astype(np.float64)
+    Y = S.simulate_panel(KIND_DNS, 150, maturities=mats).copy(order="F")
+    Y[:, [7, 40, 41, 99]] = np.nan
+    Y[0, 0] = np.nan
+    engine.set_panel(Y, mats)
+    Th = S.theta_batch(KIND_DNS, 1000 + N, seed=N, bad_frac=0.05)
+    tu = rng.integers(1, 151, Th.shape[1]).astype(np.int32)
+    a, b = both(lambda: engine.loglik(KIND_DNS, Th, T_use=tu))
+    np.testing.assert_array_equal(a, b)
+    sub = np.asfortranarray(Th[:, :40])
+    a, b = both(lambda: engine.filter_states(KIND_DNS, sub))
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
+    a, b = both(lambda: engine.predict(KIND_DNS, sub, space=0, T_use=tu[:40], horizon=3))
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    a, b = both(lambda: engine.loss_array(KIND_DNS, sub, space=0, T_use=tu[:40]))
+    np.testing.assert_array_equal(a, b)

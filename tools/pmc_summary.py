@@ -51,9 +51,10 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--evals", type=float, default=None)
     ap.add_argument("--steps", type=float, default=None)
+    ap.add_argument("--kernel", default="loglik_kernel", help="kernel-name substring to summarise")
     ap.add_argument("files", nargs="+")
     a = ap.parse_args()
-    s = summarise(a.files)
+    s = summarise(a.files, a.kernel)
     if a.evals:
         for v in s.values():
             derive(v, a.evals, a.steps)

@@ -72,7 +72,8 @@ struct DevBuf {
 // Per-launch device work buffers.  A context owns one; the estimation driver adds one per extra
 // concurrent stream (launches in flight on different streams must not share them).
 struct yfm::Workspace {
-  DevBuf flags;       // 4 × unsigned int: n_init_throw, n_neg_inf, deferral list length, n_deferred
+  DevBuf flags;       // 2 banks × 4 unsigned int: n_init_throw, n_neg_inf, deferral list length, n_deferred
+  int bank = 0;       // the bank of the last launch (the other one is zeroed by that launch's first kernel)
   DevBuf scratch;     // per-candidate work records (TVλ / GNS5 / two-wave DNS init)
   DevBuf scratch_dd;  // TVλ double-double records (YFM_PREC_CERTIFIED)
   DevBuf defer;       // candidates handed from the FP64 fixed-loading kernels to the dd kernel
@@ -89,7 +90,8 @@ struct yfm_ctx {
   DevBuf panel, mats, raw;
   // staging for host-pointer calls
   DevBuf theta, out, tuse, rec_beta, rec_P;
-  DevBuf flags;  // 4 × unsigned int: n_init_throw, n_neg_inf, deferral list length, n_deferred
+  DevBuf flags;  // 2 banks × 4 unsigned int: n_init_throw, n_neg_inf, deferral list length, n_deferred
+  int bank = 0;  // the bank of the last launch (the other one is zeroed by that launch's first kernel)
   DevBuf scratch;  // per-candidate work records (TVλ init)
   DevBuf scratch_dd;  // TVλ double-double records (YFM_PREC_CERTIFIED)
   DevBuf traj, init_bad;       // trajectory-mode state records, per-candidate init-throw marks
@@ -197,17 +199,26 @@ int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int 
            double* d_out, double* d_rb, double* d_rP, hipStream_t s, int horizon = 0, int rec_len = 0,
            const PanelView* pv = nullptr, bool reset_flags = true, yfm::Workspace* ws = nullptr) {
   DevBuf& w_flags = ws ? ws->flags : ctx->flags;
+  int& w_bank = ws ? ws->bank : ctx->bank;
   DevBuf& w_scratch = ws ? ws->scratch : ctx->scratch;
   DevBuf& w_scratch_dd = ws ? ws->scratch_dd : ctx->scratch_dd;
   DevBuf& w_defer = ws ? ws->defer : ctx->defer;
   DevBuf& w_scratch_fd = ws ? ws->scratch_fd : ctx->scratch_fd;
-  // one fill resets the flag counters (unless a pipelined chunk continues them) and this launch's
-  // deferral list length: flags.p = [n_init_throw, n_neg_inf, defer_count, n_deferred]
-  {
-    unsigned int* f = static_cast<unsigned int*>(w_flags.p);
-    YFM_HIP_CHECK(hipMemsetAsync(reset_flags ? f : f + 2, 0, (reset_flags ? 4 : 1) * sizeof(unsigned int), s));
+  // Counters [n_init_throw, n_neg_inf, defer_count, n_deferred] in two banks: a launch uses the bank
+  // its predecessor zeroed (its first kernel zeroes the other one), so no memset is enqueued per call.
+  // A pipelined chunk continues its batch's counters and only resets the deferral list length.
+  unsigned int* fb = static_cast<unsigned int*>(w_flags.p);
+  unsigned int* flags_next = nullptr;
+  if (reset_flags) {
+    w_bank ^= 1;
+    flags_next = fb + 4 * (w_bank ^ 1);
+  } else {
+    YFM_HIP_CHECK(hipMemsetAsync(fb + 4 * w_bank + 2, 0, sizeof(unsigned int), s));
   }
-  if (B == 0) return YFM_OK;
+  if (B == 0) {  // no kernel runs: zero both banks here
+    YFM_HIP_CHECK(hipMemsetAsync(fb, 0, 8 * sizeof(unsigned int), s));
+    return YFM_OK;
+  }
   yfm::LaunchArgs a;
   a.theta = d_theta;
   a.P = P;
@@ -222,7 +233,8 @@ int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int 
   a.mats = static_cast<const double*>(ctx->mats.p);
   a.T_use = d_T_use;
   a.out = d_out;
-  a.flags = static_cast<unsigned int*>(w_flags.p);
+  a.flags = fb + 4 * w_bank;
+  a.flags_next = flags_next;
   a.rec_beta = d_rb;
   a.rec_P = d_rP;
   a.scratch = nullptr;
@@ -260,7 +272,7 @@ int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int 
     // the candidates with an ill-conditioned Z'Z, which the double-double kernel then evaluates
     YFM_HIP_CHECK(w_defer.ensure(sizeof(int) * (size_t)B));
     YFM_HIP_CHECK(w_scratch_fd.ensure(yfm::fixedz_dd_scratch_bytes(kind, B)));
-    a.defer_count = reinterpret_cast<int*>(static_cast<unsigned int*>(w_flags.p) + 2);  // zeroed above
+    a.defer_count = reinterpret_cast<int*>(a.flags + 2);  // zero (a fresh bank, or reset above)
     a.defer_list = static_cast<int*>(w_defer.p);
     if (yfm::fixedz_np_for(ctx->N) > 0) {
       if (const size_t sb = yfm::fixedz_scratch_bytes(kind, B)) {
@@ -375,12 +387,12 @@ yfm_ctx* yfm_create(int hip_device) {
   yfm_ctx* ctx = new yfm_ctx();
   ctx->device = hip_device;
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
-      ctx->flags.ensure(4 * sizeof(unsigned int)) != hipSuccess) {
+      ctx->flags.ensure(8 * sizeof(unsigned int)) != hipSuccess) {
     set_error(YFM_EHIP, "context allocation failed on device %d", hip_device);
     yfm_destroy(ctx);
     return nullptr;
   }
-  (void)hipMemset(ctx->flags.p, 0, 4 * sizeof(unsigned int));
+  (void)hipMemset(ctx->flags.p, 0, 8 * sizeof(unsigned int));
   return ctx;
 }
 
@@ -570,7 +582,7 @@ int yfm_filter_states(yfm_ctx* ctx, int model_kind, int param_space, const doubl
 int yfm_last_batch_flags(yfm_ctx* ctx, long long* n_init_throw, long long* n_neg_inf) {
   if (int r = check_ctx(ctx)) return r;
   unsigned int h[2] = {0, 0};
-  YFM_HIP_CHECK(hipMemcpy(h, ctx->flags.p, sizeof(h), hipMemcpyDeviceToHost));
+  YFM_HIP_CHECK(hipMemcpy(h, static_cast<unsigned int*>(ctx->flags.p) + 4 * ctx->bank, sizeof(h), hipMemcpyDeviceToHost));
   if (n_init_throw) *n_init_throw = h[0];
   if (n_neg_inf) *n_neg_inf = h[1];
   return YFM_OK;
@@ -579,7 +591,7 @@ int yfm_last_batch_flags(yfm_ctx* ctx, long long* n_init_throw, long long* n_neg
 int yfm_last_batch_deferred(yfm_ctx* ctx, long long* n_deferred) {
   if (int r = check_ctx(ctx)) return r;
   unsigned int h[4] = {0, 0, 0, 0};
-  YFM_HIP_CHECK(hipMemcpy(h, ctx->flags.p, sizeof(h), hipMemcpyDeviceToHost));
+  YFM_HIP_CHECK(hipMemcpy(h, static_cast<unsigned int*>(ctx->flags.p) + 4 * ctx->bank, sizeof(h), hipMemcpyDeviceToHost));
   if (n_deferred) *n_deferred = h[3];
   return YFM_OK;
 }
@@ -679,12 +691,13 @@ int yfm_loss_array(yfm_ctx* ctx, int model_kind, int param_space, const double* 
   }
   const int rec_len = pv.T - 1;
   if (int r = run_trajectory(ctx, model_kind, param_space, d_th, P, B, d_tu, 0, rec_len, &pv)) return r;
-  YFM_HIP_CHECK(hipMemsetAsync(ctx->flags.p, 0, 2 * sizeof(unsigned int), ctx->stream));
+  unsigned int* cur = static_cast<unsigned int*>(ctx->flags.p) + 4 * ctx->bank;
+  YFM_HIP_CHECK(hipMemsetAsync(cur, 0, 2 * sizeof(unsigned int), ctx->stream));
   YFM_HIP_CHECK(ctx->rec_P.ensure(sizeof(double) * (size_t)T1 * B));
   yfm::PredictArgs a = predict_args(ctx, model_kind, d_th, P, B, d_tu, 1, rec_len);
   a.preds = static_cast<double*>(ctx->rec_P.p);
   YFM_HIP_CHECK(yfm::launch_loss_array(a, static_cast<const double*>(ctx->raw.p), T1, K,
-                                       static_cast<unsigned int*>(ctx->flags.p)));
+                                       cur));
   YFM_HIP_CHECK(hipMemcpyAsync(mse_out, a.preds, sizeof(double) * (size_t)T1 * B, hipMemcpyDeviceToHost, ctx->stream));
   YFM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
   return YFM_OK;
@@ -696,8 +709,8 @@ namespace yfm {
 
 Workspace* workspace_create() {
   auto* w = new Workspace;
-  if (w->flags.ensure(4 * sizeof(unsigned int)) != hipSuccess ||
-      hipMemset(w->flags.p, 0, 4 * sizeof(unsigned int)) != hipSuccess) {
+  if (w->flags.ensure(8 * sizeof(unsigned int)) != hipSuccess ||
+      hipMemset(w->flags.p, 0, 8 * sizeof(unsigned int)) != hipSuccess) {
     delete w;
     return nullptr;
   }

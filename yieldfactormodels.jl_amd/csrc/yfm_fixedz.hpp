@@ -14,13 +14,43 @@
 
 namespace yfm {
 
-// Collapsed-form measurement update (see the header): returns det S and q = v'F⁻¹v,
-// writes β_{t|t} (bf) and the upper triangle of P_{t|t} (Pf).
+// The collapsed-form measurement update in two halves:
+//   covariance (data-independent): S = P + R, its LDLᵀ and det S, P_{t|t} = P S⁻¹R;
+//   mean: ĉ, the residual ‖ỹ − Zĉ‖², c = ĉ − β, x = S⁻¹c, q = v'F⁻¹v, β_{t|t} = β + P x.
+// collapsed_update runs both in one lane; the two-wave DNS kernel (yfm_split.hip) runs them on
+// different waves, the mean wave reading (L, 1/d, P, det S) from the covariance wave.  Each value
+// has the same expression in both, so the two kernels give the same bits.
 template <int M>
-__device__ __forceinline__ void collapsed_update(const double (&zt)[M - 1], double ybar, double ytt,
-                                                 const double (&R)[M][M], double rsig2, const double (&beta)[M],
-                                                 const double (&Pm)[M][M], double (&bf)[M], double (&Pf)[M][M],
-                                                 double& det, double& q) {
+__device__ __forceinline__ double collapsed_cov(const double (&R)[M][M], const double (&Pm)[M][M], LDLT<M>& f,
+                                                double (&Pf)[M][M]) {
+  double S[M][M];
+#pragma unroll
+  for (int i = 0; i < M; ++i)
+#pragma unroll
+    for (int j = 0; j <= i; ++j) S[i][j] = Pm[i][j] + R[i][j];  // LDLᵀ reads the lower triangle only
+  const double det = f.factor(S);
+  // right-hand sides streamed one at a time: S⁻¹R column by column
+#pragma unroll
+  for (int j = 0; j < M; ++j) {
+    double xj[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) xj[i] = R[i][j];
+    f.solve(xj);
+#pragma unroll
+    for (int i = 0; i <= j; ++i) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < M; ++k) s = fma(Pm[i][k], xj[k], s);
+      Pf[i][j] = s;
+    }
+  }
+  return det;
+}
+
+template <int M>
+__device__ __forceinline__ void collapsed_mean(const double (&zt)[M - 1], double ybar, double ytt, const double (&R)[M][M],
+                                               double rsig2, const double (&beta)[M], const double (&Pm)[M][M],
+                                               const LDLT<M>& f, double (&bf)[M], double& q) {
   double zs[M - 1];
 #pragma unroll
   for (int j = 0; j < M - 1; ++j) zs[j] = zt[j] * rsig2;
@@ -36,21 +66,13 @@ __device__ __forceinline__ void collapsed_update(const double (&zt)[M - 1], doub
 #pragma unroll
   for (int j = 1; j < M; ++j) rr = fma(-zt[j - 1], ch[j], rr);
   ch[0] += ybar;
-  double S[M][M];
-  double c[M];
+  double c[M], x[M];
 #pragma unroll
   for (int i = 0; i < M; ++i) {
     c[i] = ch[i] - beta[i];
-#pragma unroll
-    for (int j = 0; j <= i; ++j) S[i][j] = Pm[i][j] + R[i][j];  // LDLᵀ reads the lower triangle only
+    x[i] = c[i];
   }
-  LDLT<M> f;
-  det = f.factor(S);
-  // right-hand sides streamed one at a time: x = S⁻¹c, then S⁻¹R column by column
-  double x[M];
-#pragma unroll
-  for (int i = 0; i < M; ++i) x[i] = c[i];
-  f.solve(x);
+  f.solve(x);  // x = S⁻¹c
   double cx = 0.0;
 #pragma unroll
   for (int i = 0; i < M; ++i) cx = fma(c[i], x[i], cx);
@@ -62,20 +84,18 @@ __device__ __forceinline__ void collapsed_update(const double (&zt)[M - 1], doub
     for (int k = 0; k < M; ++k) s = fma(Pm[i][k], x[k], s);
     bf[i] = s;
   }
-#pragma unroll
-  for (int j = 0; j < M; ++j) {
-    double xj[M];
-#pragma unroll
-    for (int i = 0; i < M; ++i) xj[i] = R[i][j];
-    f.solve(xj);
-#pragma unroll
-    for (int i = 0; i <= j; ++i) {
-      double s = 0.0;
-#pragma unroll
-      for (int k = 0; k < M; ++k) s = fma(Pm[i][k], xj[k], s);
-      Pf[i][j] = s;
-    }
-  }
+}
+
+// Collapsed-form measurement update (see the header): returns det S and q = v'F⁻¹v,
+// writes β_{t|t} (bf) and the upper triangle of P_{t|t} (Pf).
+template <int M>
+__device__ __forceinline__ void collapsed_update(const double (&zt)[M - 1], double ybar, double ytt,
+                                                 const double (&R)[M][M], double rsig2, const double (&beta)[M],
+                                                 const double (&Pm)[M][M], double (&bf)[M], double (&Pf)[M][M],
+                                                 double& det, double& q) {
+  LDLT<M> f;
+  det = collapsed_cov<M>(R, Pm, f, Pf);
+  collapsed_mean<M>(zt, ybar, ytt, R, rsig2, beta, Pm, f, bf, q);
 }
 
 

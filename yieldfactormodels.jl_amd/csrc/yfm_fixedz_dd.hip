@@ -34,6 +34,8 @@
 #include "yfm_device.hpp"
 #include "yfm_internal.hpp"
 
+#include <algorithm>
+
 namespace yfm {
 
 namespace {
@@ -112,8 +114,8 @@ __global__ __launch_bounds__(64) void fixedz_dd_init_kernel(const double* __rest
                                                             const int* __restrict__ defer_count,
                                                             double* __restrict__ rec) {
   using R = FdRec<M>;
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= *defer_count) return;
+  const int nd = *defer_count;
+  for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < nd; g += gridDim.x * blockDim.x) {
   const double* th = theta + (size_t)defer_list[g] * P + LEAD;
   double* r = rec + (size_t)g * R::Len;
   int k = 0;
@@ -206,6 +208,7 @@ __global__ __launch_bounds__(64) void fixedz_dd_init_kernel(const double* __rest
   }
   r[R::Ok] = ok ? 1.0 : 0.0;
   r[R::Ok + 1] = 0.0;
+  }
 }
 
 template <int L, int M, int LEAD, bool RECORD>
@@ -228,11 +231,12 @@ __global__ __launch_bounds__(kFdBlock) void fixedz_dd_loglik_kernel(
   __shared__ int s_nobs_max;
 
   const int nd = *defer_count;
-  if ((int)blockIdx.x * GPB >= nd) return;  // whole block past the list (before any barrier)
   const int tid = threadIdx.x;
   const int j = tid % L;
   const int grp = tid / L;
-  const int g = blockIdx.x * GPB + grp;
+  // a small grid walks the deferral list (the list is usually empty: the launch must cost ~nothing)
+  for (int base = blockIdx.x * GPB; base < nd; base += gridDim.x * GPB) {  // block-uniform bound
+  const int g = base + grp;
   const bool live = g < nd;
   const int gg = live ? g : 0;
   const int b = defer_list[gg];
@@ -449,7 +453,7 @@ __global__ __launch_bounds__(kFdBlock) void fixedz_dd_loglik_kernel(
     }
   }
 
-  if (!live || j != 0) return;
+  if (live && j == 0) {
   atomicAdd(&flags[3], 1u);  // n_deferred (yfm_last_batch_deferred)
   double ll;
   if (!init_ok) {
@@ -472,6 +476,9 @@ __global__ __launch_bounds__(kFdBlock) void fixedz_dd_loglik_kernel(
     }
   }
   out[b] = ll;
+  }
+  __syncthreads();  // LDS (panel chunks, per-group parameters) reused by the next slot group
+  }
 }
 
 namespace {
@@ -479,7 +486,7 @@ namespace {
 template <int L, int M, int LEAD>
 hipError_t launch_fd_l(const LaunchArgs& a, const double* rec, int TC) {
   constexpr int GPB = kFdBlock / L;
-  const int grid = (a.B + GPB - 1) / GPB;
+  const int grid = std::min((a.B + GPB - 1) / GPB, 256);
   const size_t shmem = sizeof(double) * ((size_t)TC + (size_t)TC * a.N + (size_t)GPB * FdRec<M>::Par);
   if (shmem > 64 * 1024) return hipErrorInvalidValue;
   if (a.rec_beta) {
@@ -496,7 +503,7 @@ hipError_t launch_fd_l(const LaunchArgs& a, const double* rec, int TC) {
 
 template <int M, int LEAD>
 hipError_t launch_fd_m(const LaunchArgs& a, double* rec) {
-  hipLaunchKernelGGL((fixedz_dd_init_kernel<M, LEAD>), dim3((a.B + 63) / 64), dim3(64), 0, a.stream, a.theta, a.P,
+  hipLaunchKernelGGL((fixedz_dd_init_kernel<M, LEAD>), dim3(std::min((a.B + 63) / 64, 64)), dim3(64), 0, a.stream, a.theta, a.P,
                      a.space, a.defer_list, a.defer_count, rec);
   if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
   constexpr int MPL = M >= 5 ? 8 : 16;

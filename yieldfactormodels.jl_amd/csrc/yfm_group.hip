@@ -37,7 +37,8 @@ __global__ __launch_bounds__(kGBlock, 2) void fixedz_group_kernel(
     const double* __restrict__ theta, int P, int B, int space, const double* __restrict__ panel, int ldp, int np,
     int T, int N, int TC, const double* __restrict__ mats, const int* __restrict__ T_use, double* __restrict__ out,
     unsigned int* __restrict__ flags, double* __restrict__ rec_beta, double* __restrict__ rec_P, int horizon,
-    int rec_len, int* __restrict__ defer_list, int* __restrict__ defer_count) {
+    int rec_len, int* __restrict__ defer_list, int* __restrict__ defer_count, unsigned int* __restrict__ flags_next) {
+  if (flags_next && blockIdx.x == 0 && threadIdx.x < 4) flags_next[threadIdx.x] = 0u;  // the next launch's counters
   constexpr int NZ = M - 1;
   constexpr int GPB = kGBlock / L;  // filters per block
   constexpr int MPL = group_max_per_lane<M>();
@@ -179,11 +180,11 @@ hipError_t launch_group_l(const LaunchArgs& a, int TC) {
   if (a.rec_beta) {
     hipLaunchKernelGGL((fixedz_group_kernel<L, M, LEAD, true>), dim3(grid), dim3(kGBlock), shmem, a.stream, a.theta,
                        a.P, a.B, a.space, a.panel, a.ldp, a.np, a.T, a.N, TC, a.mats, a.T_use, a.out, a.flags,
-                       a.rec_beta, a.rec_P, a.horizon, a.rec_len, a.defer_list, a.defer_count);
+                       a.rec_beta, a.rec_P, a.horizon, a.rec_len, a.defer_list, a.defer_count, a.flags_next);
   } else {
     hipLaunchKernelGGL((fixedz_group_kernel<L, M, LEAD, false>), dim3(grid), dim3(kGBlock), shmem, a.stream, a.theta,
                        a.P, a.B, a.space, a.panel, a.ldp, a.np, a.T, a.N, TC, a.mats, a.T_use, a.out, a.flags,
-                       nullptr, nullptr, 0, 0, a.defer_list, a.defer_count);
+                       nullptr, nullptr, 0, 0, a.defer_list, a.defer_count, a.flags_next);
   }
   return hipGetLastError();
 }

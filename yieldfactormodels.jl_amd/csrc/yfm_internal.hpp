@@ -15,7 +15,8 @@ struct LaunchArgs {
   const double* mats;   // N device
   const int* T_use;     // B device or nullptr
   double* out;          // B device
-  unsigned int* flags;  // 2 device counters
+  unsigned int* flags;  // this launch's 4 counters [n_init_throw, n_neg_inf, defer list length, n_deferred]
+  unsigned int* flags_next = nullptr;  // the other counter bank: zeroed by this launch's first kernel
   double* rec_beta;     // optional trajectories
   double* rec_P;
   double* scratch;      // per-candidate work records (tvl_scratch_bytes, fixedz_scratch_bytes)
@@ -29,6 +30,9 @@ struct LaunchArgs {
 // padded maturity count NP the fixed-loading kernel is instantiated for (-1: none)
 int fixedz_np_for(int N);
 hipError_t launch_fixedz(int kind, const LaunchArgs& a);
+// DNS with N ≤ 32: each filter split over a covariance wave and a mean wave (yfm_split.hip)
+bool dns_split_supported(int np);
+hipError_t launch_dns_split(const LaunchArgs& a);
 // per-candidate initial-state records of the per-lane kernel (GNS5: fixedz_init_kernel), bytes
 size_t fixedz_scratch_bytes(int kind, int B);
 // fixed-loading models with N beyond the per-lane kernel (yfm_group.hip): filter per lane group

@@ -74,7 +74,8 @@ constexpr int fz_rec_len() { return M + M * (M + 1) / 2 + 1; }
 
 template <int M, int LEAD>
 __global__ __launch_bounds__(256) void fixedz_init_kernel(const double* __restrict__ theta, int P, int B, int space,
-                                                          double* __restrict__ rec) {
+                                                          double* __restrict__ rec, unsigned int* __restrict__ flags_next) {
+  if (flags_next && blockIdx.x == 0 && threadIdx.x < 4) flags_next[threadIdx.x] = 0u;  // the next launch's counters
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   Params<M, LEAD> p;
@@ -136,7 +137,8 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     const double* __restrict__ theta, int P, int B, int space, const double* __restrict__ panel, int T, int N,
     const double* __restrict__ mats, const int* __restrict__ T_use, double* __restrict__ out,
     unsigned int* __restrict__ flags, double* __restrict__ rec_beta, double* __restrict__ rec_P, int horizon,
-    int rec_len, int* __restrict__ defer_list, int* __restrict__ defer_count, const double* __restrict__ init_rec) {
+    int rec_len, int* __restrict__ defer_list, int* __restrict__ defer_count, const double* __restrict__ init_rec,
+    unsigned int* __restrict__ flags_next) {
   constexpr int LDP = NP + 4;
   constexpr bool SPLIT_INIT = (M == 5);  // initial state from fixedz_init_kernel
   constexpr int CH = kTC * LDP;               // doubles per chunk
@@ -165,6 +167,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   __shared__ int s_nobs_max;
   __shared__ double s_rm[ZB ? NP : 1];  // 1/m_i (0 past N)
 
+  if (flags_next && blockIdx.x == 0 && threadIdx.x < 4) flags_next[threadIdx.x] = 0u;  // the next launch's counters
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -527,6 +530,8 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
 // ------------------------------------------------------------------------------------
 #include "yfm_internal.hpp"
 
+#include <cstdlib>
+
 namespace yfm {
 
 template <int NP, int M, int LEAD>
@@ -535,16 +540,16 @@ static hipError_t launch_fixedz_np(const LaunchArgs& a) {
   if constexpr (M == 5) {
     if (!a.scratch) return hipErrorInvalidValue;
     hipLaunchKernelGGL((fixedz_init_kernel<M, LEAD>), dim3(grid), dim3(kBlock), 0, a.stream, a.theta, a.P, a.B,
-                       a.space, a.scratch);
+                       a.space, a.scratch, a.flags_next);
   }
   if (a.rec_beta) {
     hipLaunchKernelGGL((fixedz_loglik_kernel<NP, M, LEAD, true>), dim3(grid), dim3(kBlock), 0, a.stream, a.theta, a.P,
                        a.B, a.space, a.panel, a.T, a.N, a.mats, a.T_use, a.out, a.flags, a.rec_beta, a.rec_P,
-                       a.horizon, a.rec_len, a.defer_list, a.defer_count, a.scratch);
+                       a.horizon, a.rec_len, a.defer_list, a.defer_count, a.scratch, M == 5 ? nullptr : a.flags_next);
   } else {
     hipLaunchKernelGGL((fixedz_loglik_kernel<NP, M, LEAD, false>), dim3(grid), dim3(kBlock), 0, a.stream, a.theta,
                        a.P, a.B, a.space, a.panel, a.T, a.N, a.mats, a.T_use, a.out, a.flags, nullptr, nullptr, 0, 0,
-                       a.defer_list, a.defer_count, a.scratch);
+                       a.defer_list, a.defer_count, a.scratch, M == 5 ? nullptr : a.flags_next);
   }
   return hipGetLastError();
 }
@@ -565,6 +570,11 @@ int fixedz_np_for(int N) {
 }
 
 hipError_t launch_fixedz(int kind, const LaunchArgs& a) {
+  if (kind == 0 && dns_split_supported(a.np)) {
+    // the two-wave kernel (yfm_split.hip) is measured slower on MI355X: opt-in only
+    const char* e = std::getenv("YFM_DNS_SPLIT");
+    if (e && e[0] == '1') return launch_dns_split(a);
+  }
   if (kind == 0) {
     switch (a.np) {
       case 8: return launch_fixedz_np<8, 3, 1>(a);

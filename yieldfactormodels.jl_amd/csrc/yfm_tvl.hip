@@ -52,7 +52,8 @@ enum : int { S2 = 0, S3, S4, G22, G23, G24, G33, G34, G44, U1, U2, U3, U4, VV, N
 
 // decode θ_b (transform_params + set_params!) and run initialize_filter (filter.jl:1-10)
 __global__ __launch_bounds__(256) void tvl_init_kernel(const double* __restrict__ theta, int P, int B, int space,
-                                                       double* __restrict__ rec) {
+                                                       double* __restrict__ rec, unsigned int* __restrict__ flags_next) {
+  if (flags_next && blockIdx.x == 0 && threadIdx.x < 4) flags_next[threadIdx.x] = 0u;  // the next launch's counters
   constexpr int M = 4;
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
@@ -385,7 +386,7 @@ hipError_t launch_tvl_l(const LaunchArgs& a, const TvlGaps& g, int TC) {
   const int grid = (a.B + GPB - 1) / GPB;
   const size_t shmem = sizeof(double) * (size_t)(2 * a.N + TC + TC * a.N + GPB * kTvlGaps) + sizeof(int) * a.N;
   hipLaunchKernelGGL(tvl_init_kernel, dim3((a.B + 255) / 256), dim3(256), 0, a.stream, a.theta, a.P, a.B, a.space,
-                     a.scratch);
+                     a.scratch, a.flags_next);
   if (a.rec_beta) {
     hipLaunchKernelGGL((tvl_loglik_kernel<L, true>), dim3(grid), dim3(kTvlBlock), shmem, a.stream, a.scratch, a.B,
                        a.raw, a.panel, a.ldp, a.np, a.T, a.N, TC, a.mats, g.K, g.d, g.idx, a.T_use, a.out, a.flags, a.rec_beta,

@@ -90,7 +90,8 @@ __device__ __forceinline__ void dd_propagate(const double* par, const dd (&b)[M4
 
 // decode θ_b in dd (transform_params + set_params!) and run initialize_filter (filter.jl:1-10)
 __global__ __launch_bounds__(64) void tvl_dd_init_kernel(const double* __restrict__ theta, int P, int B, int space,
-                                                         double* __restrict__ rec) {
+                                                         double* __restrict__ rec, unsigned int* __restrict__ flags_next) {
+  if (flags_next && blockIdx.x == 0 && threadIdx.x < 4) flags_next[threadIdx.x] = 0u;  // the next launch's counters
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const double* th = theta + (size_t)b * P;
@@ -578,7 +579,7 @@ int tvl_dd_lanes_for(int B, int N, int want) {
 
 hipError_t launch_tvl_dd_init(const LaunchArgs& a, double* rec_dd) {
   hipLaunchKernelGGL(tvl_dd_init_kernel, dim3((a.B + 63) / 64), dim3(64), 0, a.stream, a.theta, a.P, a.B, a.space,
-                     rec_dd);
+                     rec_dd, a.flags_next);
   hipLaunchKernelGGL(tvl_dd_colsum_kernel, dim3((a.T + 63) / 64), dim3(64), 0, a.stream, a.raw, a.N, a.T,
                      rec_dd + (size_t)kDRecLen * (size_t)(a.B > 0 ? a.B : 1));
   return hipGetLastError();
