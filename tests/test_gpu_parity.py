@@ -267,3 +267,20 @@ def test_pinned_host_buffers(engine, headline):
     assert got is out
     np.testing.assert_array_equal(out, ref)
     del th_pin, out, got
+
+
+@pytest.mark.parametrize("kind", [KIND_DNS, KIND_GNS])
+@pytest.mark.parametrize("N", [5, 12, 20, 30, 31, 40, 60])
+def test_every_panel_width_instantiation(engine, kind, N):
+    """Every padded width the per-lane kernel is instantiated for (NP = 8, 16, 24, 30, 32, 48, 64;
+    MFMA Z'ỹ up to 32, VALU dot products above) for both fixed-loading models vs the dense oracle,
+    adjudicated by the binary128 truth.  (Round 3: a register-spilling instantiation (GNS5, NP = 48)
+    computed wrong values with the update split into two functions — this pins every width.)"""
+    from oracle.truth import loglik_oracle, loglik_truth
+    rng = np.random.default_rng(N + 100 * kind)
+    mats = np.sort(rng.choice(np.arange(3, 361), N, replace=False)).astype(np.float64)
+    Y = S.simulate_panel(kind, 80, maturities=mats)
+    Th = S.theta_batch(kind, 256, seed=N, bad_frac=0.02, scale=0.05)
+    engine.set_panel(Y, mats)
+    got = engine.loglik(kind, Th)
+    assert_parity(got, loglik_oracle(kind, Y, mats, Th), loglik_truth(kind, Y, mats, Th))

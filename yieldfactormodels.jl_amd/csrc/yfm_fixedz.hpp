@@ -87,15 +87,68 @@ __device__ __forceinline__ void collapsed_mean(const double (&zt)[M - 1], double
 }
 
 // Collapsed-form measurement update (see the header): returns det S and q = v'F⁻¹v,
-// writes β_{t|t} (bf) and the upper triangle of P_{t|t} (Pf).
+// writes β_{t|t} (bf) and the upper triangle of P_{t|t} (Pf).  The same arithmetic as
+// collapsed_cov + collapsed_mean, as one body (the per-lane kernels keep this form).
 template <int M>
 __device__ __forceinline__ void collapsed_update(const double (&zt)[M - 1], double ybar, double ytt,
                                                  const double (&R)[M][M], double rsig2, const double (&beta)[M],
                                                  const double (&Pm)[M][M], double (&bf)[M], double (&Pf)[M][M],
                                                  double& det, double& q) {
+  double zs[M - 1];
+#pragma unroll
+  for (int j = 0; j < M - 1; ++j) zs[j] = zt[j] * rsig2;
+  double ch[M];  // ĉ = G⁻¹(0, z̃) (= R/σ² · (0, z̃))
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    double s = 0.0;
+#pragma unroll
+    for (int j = 1; j < M; ++j) s = fma(R[i][j], zs[j - 1], s);
+    ch[i] = s;
+  }
+  double rr = ytt;  // ‖ỹ − Zĉ‖² = ỹ'ỹ − z̃'ĉ
+#pragma unroll
+  for (int j = 1; j < M; ++j) rr = fma(-zt[j - 1], ch[j], rr);
+  ch[0] += ybar;
+  double S[M][M];
+  double c[M];
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    c[i] = ch[i] - beta[i];
+#pragma unroll
+    for (int j = 0; j <= i; ++j) S[i][j] = Pm[i][j] + R[i][j];  // LDLᵀ reads the lower triangle only
+  }
   LDLT<M> f;
-  det = collapsed_cov<M>(R, Pm, f, Pf);
-  collapsed_mean<M>(zt, ybar, ytt, R, rsig2, beta, Pm, f, bf, q);
+  det = f.factor(S);
+  // right-hand sides streamed one at a time: x = S⁻¹c, then S⁻¹R column by column
+  double x[M];
+#pragma unroll
+  for (int i = 0; i < M; ++i) x[i] = c[i];
+  f.solve(x);
+  double cx = 0.0;
+#pragma unroll
+  for (int i = 0; i < M; ++i) cx = fma(c[i], x[i], cx);
+  q = fma(rr, rsig2, cx);
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    double s = beta[i];
+#pragma unroll
+    for (int k = 0; k < M; ++k) s = fma(Pm[i][k], x[k], s);
+    bf[i] = s;
+  }
+#pragma unroll
+  for (int j = 0; j < M; ++j) {
+    double xj[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) xj[i] = R[i][j];
+    f.solve(xj);
+#pragma unroll
+    for (int i = 0; i <= j; ++i) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < M; ++k) s = fma(Pm[i][k], xj[k], s);
+      Pf[i][j] = s;
+    }
+  }
 }
 
 
