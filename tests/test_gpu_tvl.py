@@ -139,6 +139,52 @@ def test_tvl_config3_sample_fp64(engine, config3):
     assert np.median(rel(got, tru)) <= max(np.median(rel(ora, tru)), 1e-13)
 
 
+@pytest.fixture(scope="module")
+def config3_1024():
+    mats = S.maturities_360()
+    Y = S.simulate_panel(KIND_TVL, 600, maturities=mats)
+    with np.load(GOLDEN / "config3" / "tvl_config3_1024.npz", allow_pickle=False) as z:
+        fx = {k: z[k] for k in z.files}
+    return Y, mats, fx
+
+
+def test_tvl_config3_1024_certified(engine, config3_1024):
+    """The certified filter on 1,024 config-3 candidates: factor-1 parity on every one, and every
+    candidate within 1e-9 of the binary128 truth — where the reference's dense FP64 path (the oracle)
+    is up to 1.1e-2 from exact arithmetic on this sample (tests/golden/config3/make_tvl_config3_1024.py).
+    (A few candidates amplify rounding by up to ~1e20, so even double-double lands up to ~1e-10 from
+    the truth there — 5 of the 1,012 finite ones above 1e-13, for the round-2 kernel as for this one,
+    profiles/r3/tvl_dd_ab; the rest reproduce it to ~1e-13.)"""
+    Y, mats, fx = config3_1024
+    engine.set_panel(Y, mats)
+    got = engine.loglik(KIND_TVL, fx["Theta"])
+    table = assert_parity(got, fx["loglik_oracle"], fx["loglik_truth"])
+    e = rel(got, fx["loglik_truth"])
+    print("certified 1024", table, "max rel vs truth %.2e, %d above 1e-13" % (e.max(), (e > EXACT).sum()))
+    assert table["failing"] == 0
+    assert e.max() <= 1e-9 and (e > EXACT).sum() <= 10
+
+
+def test_tvl_config3_1024_fp64_reference_class(engine, config3_1024):
+    """FP64 mode is the reference's arithmetic class: on amplifying candidates every FP64 evaluation
+    (the reference's dense path included) is rounding noise around the exact value.  On 1,024
+    candidates its error against the binary128 truth must be no worse than the dense oracle's in the
+    median and at the 99th percentile, and its largest error within 2× the oracle's largest; the
+    patterns must match."""
+    Y, mats, fx = config3_1024
+    engine.set_panel(Y, mats)
+    with precision(engine, _lib.PREC_FP64):
+        got = engine.loglik(KIND_TVL, fx["Theta"])
+    ora, tru = fx["loglik_oracle"], fx["loglik_truth"]
+    assert np.array_equal(np.isfinite(got), np.isfinite(ora)) and np.array_equal(np.isnan(got), np.isnan(ora))
+    eg, eo = rel(got, tru), rel(ora, tru)
+    q = lambda e: (float(np.median(e)), float(np.quantile(e, 0.99)), float(e.max()))  # noqa: E731
+    print("fp64 1024 (median, p99, max) gpu", q(eg), "oracle", q(eo), parity_table(got, ora, tru))
+    assert np.median(eg) <= max(np.median(eo), 1e-13)
+    assert np.quantile(eg, 0.99) <= np.quantile(eo, 0.99)
+    assert eg.max() <= 2.0 * eo.max()
+
+
 def test_tvl_windows_nan_and_edges(engine, config3):
     """T_use windows, NaN columns (prediction-only steps, stale F/v re-added), tiny T."""
     Y, mats, _ = config3

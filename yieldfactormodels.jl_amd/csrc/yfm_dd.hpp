@@ -116,7 +116,40 @@ struct dd_acc {
     add(p);
   }
   __device__ __forceinline__ dd value() const { return two_sum(hi, lo); }  // |lo| may exceed |hi| after cancellation
+
+  // σ-split accumulation (Rump, Ogita & Oishi's ExtractScalar): with σ a power of two ≥ n·max|x.hi|
+  // over the n terms this accumulator will receive, q = (σ + x.hi) − σ is x.hi rounded to a multiple
+  // of ulp(σ) and x.hi − q is exact; every partial sum of the q's is a multiple of ulp(σ) below 2σ, so
+  // `hi` stays exact with one plain addition instead of a TwoSum.  The absolute error, ≈ n²·ulp(σ)·u,
+  // is in the same class as add()'s (the sums here have ≤ a few hundred terms).
+  __device__ __forceinline__ void add_sx(dd x, double sg) {
+    const double q = (sg + x.hi) - sg;
+    hi += q;
+    lo += (x.hi - q) + x.lo;
+  }
+  // += a·b: a.hi·b.hi − q to one rounding (|·| ≤ ulp(σ)), plus the cross terms
+  __device__ __forceinline__ void add_prod_sx(dd a, dd b, double sg) {
+    const double q = (sg + a.hi * b.hi) - sg;
+    hi += q;
+    lo += __builtin_fma(a.hi, b.hi, -q);
+    lo = __builtin_fma(a.hi, b.lo, lo);
+    lo = __builtin_fma(a.lo, b.hi, lo);
+  }
+  // += a·d (d a double)
+  __device__ __forceinline__ void add_prod_d_sx(dd a, double d, double sg) {
+    const double q = (sg + a.hi * d) - sg;
+    hi += q;
+    lo += __builtin_fma(a.hi, d, -q);
+    lo = __builtin_fma(a.lo, d, lo);
+  }
 };
+
+// the split constant for add_sx & co.: a power of two ≥ x (x = terms × bound on |term|); 1 for
+// x = 0 and 2^1000 for a non-finite bound (the split then degrades to FP64 accumulation into lo)
+__device__ __forceinline__ double split_const(double x) {
+  if (!(x <= 0x1p1000)) return 0x1p1000;
+  return __builtin_ldexp(1.0, __builtin_amdgcn_frexp_exp(x));
+}
 
 // exp of a dd argument to ~2u² relative: x = k·ln2 + r, |r| ≤ ln2/2, e^r from a degree-9
 // Taylor polynomial of r/2^9 followed by 9 squarings of (1 + s) carried as s ← s(2 + s).
@@ -277,6 +310,34 @@ __device__ __forceinline__ void pair_exchange(double x, double& a, double& b) {
     a = __hiloint2double(rh[0], rl[0]);
     b = __hiloint2double(rh[1], rl[1]);
   }
+}
+
+// ---- quad exchanges for the lane-distributed 4×4 update (role c = lane & 3 inside each quad) ----
+template <int CTRL>
+__device__ __forceinline__ double quad_dpp(double x) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), CTRL, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), CTRL, 0xf, 0xf, true);
+  return __hiloint2double(hi, lo);
+}
+// the value held by role S of this lane's quad
+template <int S>
+__device__ __forceinline__ dd quad_bcast(dd x) {
+  constexpr int ctrl = S | (S << 2) | (S << 4) | (S << 6);
+  return {quad_dpp<ctrl>(x.hi), quad_dpp<ctrl>(x.lo)};
+}
+// the value held by role c ^ R (R = 1, 2, 3)
+template <int R>
+__device__ __forceinline__ dd quad_xor(dd x) {
+  constexpr int ctrl = (0 ^ R) | ((1 ^ R) << 2) | ((2 ^ R) << 4) | ((3 ^ R) << 6);
+  return {quad_dpp<ctrl>(x.hi), quad_dpp<ctrl>(x.lo)};
+}
+// v[i] for a lane-dependent i in [0, 4)
+__device__ __forceinline__ dd sel4(const dd (&v)[4], int i) {
+  dd r = v[0];
+  r = i == 1 ? v[1] : r;
+  r = i == 2 ? v[2] : r;
+  r = i == 3 ? v[3] : r;
+  return r;
 }
 
 template <int LVL>

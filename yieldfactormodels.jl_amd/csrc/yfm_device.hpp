@@ -488,6 +488,34 @@ __device__ __forceinline__ double group_level_sum(double x) {
   }
 }
 
+// The value of role S (lane & 3 = S) of this lane's quad: DPP quad_perm broadcast.  Used by the
+// TVλ filters to distribute their 4×4 update over the four roles of each quad.
+template <int S>
+__device__ __forceinline__ double quad_bcast_f64(double x) {
+  constexpr int ctrl = S | (S << 2) | (S << 4) | (S << 6);
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), ctrl, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), ctrl, 0xf, 0xf, true);
+  return __hiloint2double(hi, lo);
+}
+// rows of a 4×4 whose row S lives in role S, into every lane
+template <int M>
+__device__ __forceinline__ void quad_gather_rows(const double (&row)[M], double (&X)[M][M]) {
+  static_assert(M == 4, "quad roles hold the rows of a 4×4");
+#pragma unroll
+  for (int k = 0; k < M; ++k) {
+    X[0][k] = quad_bcast_f64<0>(row[k]);
+    X[1][k] = quad_bcast_f64<1>(row[k]);
+    X[2][k] = quad_bcast_f64<2>(row[k]);
+    X[3][k] = quad_bcast_f64<3>(row[k]);
+  }
+}
+// LDS writes of this wave visible to its own later LDS reads
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Sum over the aligned group of L lanes (DPP / permlane butterflies, no LDS); every lane of
 // the group receives the total.
 template <int L>

@@ -326,6 +326,7 @@ extern "C" int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const
   if (const char* e = std::getenv("YFM_EST_THREADS")) nthreads = std::max(1, std::atoi(e));
   Pool pool(std::min(nthreads, std::max(1, R / (4 * G))));
   std::atomic<int> active{0};
+  std::atomic<int> last_active{-1};  // highest chain index of the group that requested points this round
   long long device_evals = 0, rounds = 0;
   double t_host = 0.0, t_dev = 0.0;
   using clk = std::chrono::steady_clock;
@@ -344,6 +345,8 @@ extern "C" int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const
     const auto h2 = stats ? clk::now() : clk::time_point();
     if (c.n_req > 0) {
       active.fetch_add(1, std::memory_order_relaxed);
+      for (int m = last_active.load(std::memory_order_relaxed); m < r;)
+        if (last_active.compare_exchange_weak(m, r, std::memory_order_relaxed)) break;
       double* slot = th + (size_t)r * SLOT * P;
       if (c.nodes.empty())
         std::memcpy(slot, c.trial.data(), sizeof(double) * c.trial.size());
@@ -361,14 +364,19 @@ extern "C" int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const
   int r0[kMaxGroups + 1];
   for (int g = 0; g <= G; ++g) r0[g] = (int)((long long)R * g / G);
   bool pending[kMaxGroups] = {};
+  // launch extent per group: up to the last chain that requested points (finished chains at the
+  // end of a group cost no lanes; the slots of finished chains inside it are still evaluated)
+  int r_end[kMaxGroups] = {};
   auto host_group = [&](int g) {
     active.store(0);
+    last_active.store(-1);
     pool.run(r0[g + 1] - r0[g], 2, [&](int i) { host_step(r0[g] + i); });
+    r_end[g] = last_active.load() + 1;
     return active.load() > 0;
   };
   auto submit = [&](int g) -> int {
     const size_t o = (size_t)r0[g] * SLOT;
-    const int Bg = (r0[g + 1] - r0[g]) * SLOT;
+    const int Bg = (r_end[g] - r0[g]) * SLOT;
     if (zero_copy) {
       const int rc = yfm::loglik_device_ws(ctx, wss[g], model_kind, YFM_THETA_UNCONSTRAINED, map_th + o * P, P, Bg,
                                            d_tu ? d_tu + o : nullptr, map_out + o, sts[g]);

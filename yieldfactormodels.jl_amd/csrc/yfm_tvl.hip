@@ -81,6 +81,61 @@ __global__ __launch_bounds__(256) void tvl_init_kernel(const double* __restrict_
   r[47] = 0.0;
 }
 
+// Lane-distributed 4×4 update (L ≥ 4): the four roles qr = lane & 3 of each quad hold column qr of P,
+// row qr of Φ, column qr of Q and δ_qr; the group's other quads repeat the same work.  Every
+// quantity is formed with the replicated kernel's operation order, so the results are bitwise
+// those of the one-lane-does-everything form (a role forms the upper entries (i ≤ qr) of its
+// column; entries below the diagonal come from the role that owns them as upper entries, through
+// the group's LDS exchange block).
+struct TvlQuad {
+  int qr;
+  double phr[4], qc[4], dq;
+  double* xch;  // this group's 4×4 exchange block (LDS)
+
+  // column qr of the symmetric matrix whose upper entries are `v[i]` for i ≤ qr (this role) and
+  // role k's v[qr] for k > qr
+  __device__ __forceinline__ void mirror(const double (&v)[4], double (&col)[4]) const {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) xch[qr * 4 + k] = v[k];
+    wave_lds_sync();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const double o = xch[k * 4 + qr];
+      col[k] = k <= qr ? v[k] : o;
+    }
+    wave_lds_sync();  // the block is rewritten by the next exchange
+  }
+  // β ← δ + Φ bf;  P ← Φ Pf Φ' + Q  (propagate_state, filter.jl:162-176): Pf the full symmetric matrix
+  __device__ __forceinline__ void propagate(const double (&bf)[4], const double (&Pf)[4][4], double (&beta)[4],
+                                            double (&Pc)[4]) const {
+    double bq = dq;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bq = fma(phr[j], bf[j], bq);
+    beta[0] = quad_bcast_f64<0>(bq);
+    beta[1] = quad_bcast_f64<1>(bq);
+    beta[2] = quad_bcast_f64<2>(bq);
+    beta[3] = quad_bcast_f64<3>(bq);
+    double ar[4], A[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      double a = 0.0;
+#pragma unroll
+      for (int l = 0; l < 4; ++l) a = fma(phr[l], Pf[l][j], a);
+      ar[j] = a;
+    }
+    quad_gather_rows<4>(ar, A);
+    double pc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      double t = qc[i];
+#pragma unroll
+      for (int l = 0; l < 4; ++l) t = fma(A[i][l], phr[l], t);
+      pc[i] = t;
+    }
+    mirror(pc, Pc);
+  }
+};
+
 template <int L, bool RECORD>
 __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
     const double* __restrict__ rec, int B, const double* __restrict__ Y,
@@ -95,7 +150,8 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
   double* s_nan = smem + 2 * N;                       // TC NaN flags of the staged chunk
   double* s_y = s_nan + TC;                           // TC columns of N yields (column-major, stride N)
   double* s_w = s_y + TC * N;                         // per group: e^{-λ d_k}, k < K (≤ kTvlGaps)
-  int* s_gi = reinterpret_cast<int*>(s_w + GPB * kTvlGaps);  // gap index of the jump i → i + L
+  double* s_xch = s_w + GPB * kTvlGaps;               // per group: 4×4 exchange block (L ≥ 4)
+  int* s_gi = reinterpret_cast<int*>(s_xch + (L >= 4 ? GPB * 16 : 0));  // gap index of the jump i → i + L
   __shared__ double s_gd[kTvlGaps];
   __shared__ int s_nobs_max;
 
@@ -121,10 +177,29 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
   const int my_data = horizon > 0 ? nobs : nobs - 1;
   atomicMax(&s_nobs_max, live ? my_steps : 0);
 
+  constexpr bool DIST = L >= 4;  // distributed 4×4 update (TvlQuad)
   Params<M, 0> p;
   double beta[M], Pm[M][M];
+  TvlQuad qd;
+  double Pc[M];  // DIST: column qr of P
   bool init_ok;
-  {
+  if constexpr (DIST) {
+    const double* r = rec + (size_t)bb * kRecLen;
+    qd.qr = tid & 3;
+    qd.xch = s_xch + grp * 16;
+    qd.dq = r[kRecDelta + qd.qr];
+    p.sigma2 = r[kRecSigma];
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      beta[i] = r[kRecBeta + i];
+      qd.phr[i] = r[kRecPhi + qd.qr * M + i];
+      const int lo = i < qd.qr ? i : qd.qr, hi = i < qd.qr ? qd.qr : i;
+      const int q = lo * M - lo * (lo - 1) / 2 + (hi - lo);  // upper-triangle record index
+      qd.qc[i] = r[kRecQ + q];
+      Pc[i] = r[kRecP + q];
+    }
+    init_ok = r[kRecOk] != 0.0;
+  } else {
     const double* r = rec + (size_t)bb * kRecLen;
     p.sigma2 = r[kRecSigma];
     int q = 0;
@@ -142,6 +217,7 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
     }
     init_ok = r[kRecOk] != 0.0;
   }
+  (void)Pc;
   const double sigma2 = p.sigma2;
   const double rsig2 = 1.0 / sigma2;
 
@@ -194,14 +270,22 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
     const bool nan_col = s_nan[tt] != 0.0 || t >= my_data;
     if (act && nan_col) {
       // filter.jl:13-29: prediction only; F, F⁻¹, v stale → the loglik re-adds the last term
-      double bf[M], Pf[M][M];
+      if constexpr (DIST) {
+        double bf[M], Pf[M][M];
 #pragma unroll
-      for (int i = 0; i < M; ++i) {
-        bf[i] = beta[i];
+        for (int i = 0; i < M; ++i) bf[i] = beta[i];
+        quad_gather_rows<M>(Pc, Pf);  // P symmetric: role S's column is row S
+        qd.propagate(bf, Pf, beta, Pc);
+      } else {
+        double bf[M], Pf[M][M];
 #pragma unroll
-        for (int k = i; k < M; ++k) Pf[i][k] = Pm[i][k];
+        for (int i = 0; i < M; ++i) {
+          bf[i] = beta[i];
+#pragma unroll
+          for (int k = i; k < M; ++k) Pf[i][k] = Pm[i][k];
+        }
+        propagate_state<M, 0>(p, bf, Pf, beta, Pm);
       }
-      propagate_state<M, 0>(p, bf, Pf, beta, Pm);
       if (acc) {
         ld.mul(last_det);
         sumq += last_q;
@@ -297,7 +381,91 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
       const bool upd = true;
       const double q = vv * rsig2;
 #else
-      double W[M][M], det;
+      double det, q;
+      bool upd;
+      if constexpr (DIST) {
+        // row qr of B̃ = σ²I + P G (P symmetric: row qr is the column this role holds), broadcast
+        double Ar[M], A[M][M], x[M];
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+          double t = (k == qd.qr) ? sigma2 : 0.0;
+#pragma unroll
+          for (int l = 0; l < M; ++l) t = fma(Pc[l], G[l][k], t);
+          Ar[k] = t;
+          x[k] = Pc[k];
+        }
+        quad_gather_rows<M>(Ar, A);
+        // Capacitance::solve with ONE right-hand side: column qr of P
+        double sgn = 1.0, prod = 1.0;
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+          int pv = k;
+          double amax = fabs(A[k][k]);
+#pragma unroll
+          for (int i = k + 1; i < M; ++i) {
+            const double a = fabs(A[i][k]);
+            const bool gt = a > amax;
+            amax = gt ? a : amax;
+            pv = gt ? i : pv;
+          }
+          sgn = (pv != k) ? -sgn : sgn;
+#pragma unroll
+          for (int i = k + 1; i < M; ++i) {
+            const bool sw = (pv == i);
+#pragma unroll
+            for (int c = k; c < M; ++c) {
+              const double a = A[k][c], b = A[i][c];
+              A[k][c] = sw ? b : a;
+              A[i][c] = sw ? a : b;
+            }
+            const double a = x[k], b = x[i];
+            x[k] = sw ? b : a;
+            x[i] = sw ? a : b;
+          }
+          const double piv = A[k][k];
+          prod *= piv;
+          const double rp = 1.0 / piv;
+#pragma unroll
+          for (int i = k + 1; i < M; ++i) {
+            const double l = A[i][k] * rp;
+#pragma unroll
+            for (int c = k + 1; c < M; ++c) A[i][c] = fma(-l, A[k][c], A[i][c]);
+            x[i] = fma(-l, x[k], x[i]);
+          }
+        }
+#pragma unroll
+        for (int k = M - 1; k >= 0; --k) {
+          const double rp = 1.0 / A[k][k];
+          double t = x[k];
+#pragma unroll
+          for (int j2 = k + 1; j2 < M; ++j2) t = fma(-A[k][j2], x[j2], t);
+          x[k] = t * rp;
+        }
+        det = sgn * prod;
+        // column qr of W (its upper triangle mirrored, as the replicated form uses it)
+        double wc[M];
+        qd.mirror(x, wc);
+        double wq = 0.0;
+#pragma unroll
+        for (int k = 0; k < M; ++k) wq = fma(wc[k], u[k], wq);
+        const double w[M] = {quad_bcast_f64<0>(wq), quad_bcast_f64<1>(wq), quad_bcast_f64<2>(wq), quad_bcast_f64<3>(wq)};
+        double bf[M], uk = 0.0;
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+          bf[i] = beta[i] + w[i];
+          uk = fma(u[i], w[i], uk);
+        }
+        q = (vv - uk) * rsig2;
+        upd = det != 0.0;  // inv(F) threw: return without updating (filter.jl:51-56)
+        if (upd) {
+          double pfc[M], Pf[M][M];
+#pragma unroll
+          for (int k = 0; k < M; ++k) pfc[k] = sigma2 * wc[k];
+          quad_gather_rows<M>(pfc, Pf);
+          qd.propagate(bf, Pf, beta, Pc);
+        }
+      } else {
+      double W[M][M];
 #if defined(YFM_TVL_PROBE) && YFM_TVL_PROBE == 2
       Capacitance<M>::solve(Pm, G, sigma2, W, det, &probe_swapped);  // statistics probe
 #else
@@ -316,13 +484,14 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
         bf[i] = beta[i] + w;
         uk = fma(u[i], w, uk);
       }
-      const double q = (vv - uk) * rsig2;
+      q = (vv - uk) * rsig2;
 #pragma unroll
       for (int i = 0; i < M; ++i)
 #pragma unroll
         for (int k = i; k < M; ++k) Pf[i][k] = sigma2 * W[i][k];
-      const bool upd = det != 0.0;  // inv(F) threw: return without updating (filter.jl:51-56)
+      upd = det != 0.0;  // inv(F) threw: return without updating (filter.jl:51-56)
       if (upd) propagate_state<M, 0>(p, bf, Pf, beta, Pm);
+      }
 #endif
       last_det = det;
       last_q = upd ? q : __builtin_nan("");
@@ -333,6 +502,8 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
       }
     }
     if constexpr (RECORD) {
+      double Pfull[M][M];
+      if constexpr (DIST) quad_gather_rows<M>(Pc, Pfull);  // every lane of the quad takes part
       const int slot = t - max(0, my_steps - rec_len);  // the last rec_len steps
       if (live && act && j == 0 && slot >= 0) {
         const size_t o = (size_t)b * (size_t)rec_len + slot;
@@ -342,7 +513,7 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
 #pragma unroll
           for (int k = 0; k < M; ++k)
 #pragma unroll
-            for (int i = 0; i < M; ++i) rec_P[o * M * M + k * M + i] = Pm[i][k];
+            for (int i = 0; i < M; ++i) rec_P[o * M * M + k * M + i] = DIST ? Pfull[i][k] : Pm[i][k];
         }
       }
     }
@@ -384,7 +555,8 @@ template <int L>
 hipError_t launch_tvl_l(const LaunchArgs& a, const TvlGaps& g, int TC) {
   constexpr int GPB = kTvlBlock / L;
   const int grid = (a.B + GPB - 1) / GPB;
-  const size_t shmem = sizeof(double) * (size_t)(2 * a.N + TC + TC * a.N + GPB * kTvlGaps) + sizeof(int) * a.N;
+  const size_t shmem = sizeof(double) * (size_t)(2 * a.N + TC + TC * a.N + GPB * kTvlGaps + (L >= 4 ? GPB * 16 : 0)) +
+                       sizeof(int) * a.N;
   hipLaunchKernelGGL(tvl_init_kernel, dim3((a.B + 255) / 256), dim3(256), 0, a.stream, a.theta, a.P, a.B, a.space,
                      a.scratch, a.flags_next);
   if (a.rec_beta) {

@@ -27,6 +27,10 @@
 #include "yfm_device.hpp"
 #include "yfm_internal.hpp"
 
+#ifndef YFM_DD_SPLIT_Z4
+#define YFM_DD_SPLIT_Z4 1  // 0: TwoSum accumulation for the Jacobian-column sums (A/B builds)
+#endif
+
 namespace yfm {
 
 namespace {
@@ -84,6 +88,80 @@ __device__ __forceinline__ void dd_propagate(const double* par, const dd (&b)[M4
       if (scale) s = dd_mul(s, sig2);
       P[utri(i, k)] = dd_add(s, Q[utri(i, k)]);
     }
+}
+
+// LDS writes of this wave visible to its own later reads (the quads of a filter are in one wave)
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int S>
+__device__ __forceinline__ void bcast_row(const dd (&v)[M4], dd (&out)[M4]) {
+#pragma unroll
+  for (int k = 0; k < M4; ++k) out[k] = quad_bcast<S>(v[k]);
+}
+// the symmetric 4×4 whose column `qr` each role qr of the quad holds, in every lane
+__device__ __forceinline__ void gather_sym(const dd (&col)[M4], dd (&X)[M4][M4]) {
+  bcast_row<0>(col, X[0]);
+  bcast_row<1>(col, X[1]);
+  bcast_row<2>(col, X[2]);
+  bcast_row<3>(col, X[3]);
+}
+
+// dd_propagate distributed over the quad (role qr = lane & 3; lanes of a group with the same role
+// compute the same values): β_qr then a broadcast; row qr of A = ΦX, broadcast; then column qr of
+// the new P.  Every upper entry (i ≤ k) is formed by role k exactly as dd_propagate forms it, and the
+// entry below the diagonal is taken from the role that owns it as an upper entry, so P stays bitwise
+// symmetric and bitwise dd_propagate's.  X: the full symmetric matrix (every lane).
+// xch: this filter's 4×4 dd exchange block in LDS (the transpose of the new P's columns).
+__device__ __forceinline__ void dd_propagate_q(const double* par, int qr, const dd (&b)[M4], const dd (&X)[M4][M4],
+                                               bool scale, dd* xch, dd (&beta)[M4], dd (&Pc)[M4]) {
+  const dd* Phi = reinterpret_cast<const dd*>(par + kDPhi);
+  const dd* Q = reinterpret_cast<const dd*>(par + kDQ);
+  const dd sig2 = *reinterpret_cast<const dd*>(par + kDSig);
+  {
+    dd s = dd_make(par[kDDelta + qr]);
+#pragma unroll
+    for (int j = 0; j < M4; ++j) s = dd_add(s, dd_mul(Phi[qr * M4 + j], b[j]));
+    beta[0] = quad_bcast<0>(s);
+    beta[1] = quad_bcast<1>(s);
+    beta[2] = quad_bcast<2>(s);
+    beta[3] = quad_bcast<3>(s);
+  }
+  dd A[M4][M4];
+  {
+    dd Ar[M4];
+#pragma unroll
+    for (int j = 0; j < M4; ++j) {
+      dd_acc a;
+#pragma unroll
+      for (int l = 0; l < M4; ++l) a.add_prod(Phi[qr * M4 + l], X[l][j]);
+      Ar[j] = a.value();
+    }
+    gather_sym(Ar, A);  // row i of A from role i (not symmetric: bcast_row just moves rows)
+  }
+  dd pc[M4];
+#pragma unroll
+  for (int i = 0; i < M4; ++i) {
+    dd_acc a;
+#pragma unroll
+    for (int l = 0; l < M4; ++l) a.add_prod(A[i][l], Phi[qr * M4 + l]);
+    dd s = a.value();
+    if (scale) s = dd_mul(s, sig2);
+    pc[i] = dd_add(s, Q[i <= qr ? utri(i, qr) : utri(qr, i)]);
+  }
+  // role qr's value of entry (k, qr) is its own for k ≤ qr and role k's upper entry (qr, k) below
+#pragma unroll
+  for (int k = 0; k < M4; ++k) xch[qr * M4 + k] = pc[k];
+  wave_sync();
+#pragma unroll
+  for (int k = 0; k < M4; ++k) {
+    const dd o = xch[k * M4 + qr];
+    Pc[k] = k <= qr ? pc[k] : o;
+  }
+  wave_sync();  // the block is rewritten by the next exchange
 }
 
 }  // namespace
@@ -189,18 +267,22 @@ __global__ __launch_bounds__(64) void tvl_dd_init_kernel(const double* __restric
 }
 
 // Σ_i y_it and Σ_i y_it² per panel column in dd (summed in maturity order; NaN columns give
-// NaN and are never read): colsum[4t .. 4t+3] = (Σy.hi, Σy.lo, Σy².hi, Σy².lo)
+// NaN and are never read): colsum[4t .. 4t+3] = (Σy.hi, Σy.lo, Σy².hi, Σy².lo); colsum[4T + t] =
+// max_i |y_it| (the bound of the σ-split statistics' y terms)
 __global__ __launch_bounds__(64) void tvl_dd_colsum_kernel(const double* __restrict__ Y, int N, int T,
                                                            double* __restrict__ colsum) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= T) return;
   const double* y = Y + (size_t)t * N;
   dd_acc s1, s2;
+  double ym = 0.0;
   for (int i = 0; i < N; ++i) {
     const double v = y[i];
     s1.add(dd_make(v));
     s2.add(two_prod(v, v));
+    ym = fmax(ym, fabs(v));
   }
+  colsum[4 * (size_t)T + t] = ym;
   const dd a = s1.value(), b = s2.value();
   colsum[4 * (size_t)t] = a.hi;
   colsum[4 * (size_t)t + 1] = a.lo;
@@ -221,11 +303,14 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
   dd* s_rm = reinterpret_cast<dd*>(smem + N);          // 1/m_i (dd)
   double* s_nan = smem + 3 * N;                        // TC NaN flags of the staged chunk
   dd* s_sum = reinterpret_cast<dd*>(s_nan + TC);       // per staged column: Σy, Σy² (dd)
-  double* s_y = s_nan + 5 * TC;                        // TC columns of N yields
+  double* s_ymax = s_nan + 5 * TC;                     // per staged column: max_i |y_i|
+  double* s_y = s_nan + 6 * TC;                        // TC columns of N yields
   double* s_par = s_y + TC * N;                        // per group: σ², δ, Φ, Q (kDPar doubles)
   dd* s_w = reinterpret_cast<dd*>(s_par + GPB * kDPar);  // per group: e^{-λ d_k}, k < K
-  int* s_gi = reinterpret_cast<int*>(s_w + GPB * kDdWStride);
+  dd* s_xch = s_w + GPB * kDdWStride;                  // per group: 4×4 dd exchange block
+  int* s_gi = reinterpret_cast<int*>(s_xch + GPB * M4 * M4);
   __shared__ double s_gd[kTvlGaps];
+  __shared__ int s_gsrc[kTvlGaps];  // a lane whose first maturity equals jump k exactly, or −1
   __shared__ int s_nobs_max;
 
   const int tid = threadIdx.x;
@@ -243,20 +328,38 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
     s_rm[i] = dd_rcp(dd_make(m));
     if (K > 0) s_gi[i] = gap_idx[i];
   }
-  if (tid < K) s_gd[tid] = gap_d[tid];
+  if (tid < K) {
+    const double d = gap_d[tid];
+    s_gd[tid] = d;
+    int src = -1;
+    for (int q = min(L, N) - 1; q >= 0; --q) src = mats[q] == d ? q : src;
+    s_gsrc[tid] = src;
+  }
   const double* r = rec + (size_t)bb * kDRecLen;
   double* par = s_par + grp * kDPar;
   for (int q = j; q < kDPar; q += L) par[q] = r[q];
   __syncthreads();
+  // this lane's maturities i ≡ j (mod L): count and smallest maturity (bounds of the σ-split sums)
+  double l_n = 0.0, l_minm = __builtin_inf();
+  for (int i = j; i < N; i += L) {
+    l_n += 1.0;
+    l_minm = fmin(l_minm, s_m[i]);
+  }
+  const double l_rminm = 1.0 / l_minm;
   const int my_steps = horizon > 0 ? nobs + horizon : nobs - 1;
   const int my_data = horizon > 0 ? nobs : nobs - 1;
   atomicMax(&s_nobs_max, live ? my_steps : 0);
 
-  dd beta[M4], Pm[10];
+  // the 4×4 update is distributed over the lanes of each quad: role qr holds column qr of P
+  const int qr = tid & 3;
+  dd* xch = s_xch + grp * M4 * M4;
+  dd beta[M4], Pc[M4];
 #pragma unroll
-  for (int i = 0; i < M4; ++i) beta[i] = {r[kDBeta + 2 * i], r[kDBeta + 2 * i + 1]};
-#pragma unroll
-  for (int q = 0; q < 10; ++q) Pm[q] = {r[kDP + 2 * q], r[kDP + 2 * q + 1]};
+  for (int i = 0; i < M4; ++i) {
+    beta[i] = {r[kDBeta + 2 * i], r[kDBeta + 2 * i + 1]};
+    const int q = i <= qr ? utri(i, qr) : utri(qr, i);
+    Pc[i] = {r[kDP + 2 * q], r[kDP + 2 * q + 1]};
+  }
   const bool init_ok = r[kDOk] != 0.0;
   const dd sig2 = {par[kDSig], par[kDSig + 1]};
   const dd rsig2 = dd_rcp(sig2);
@@ -271,7 +374,7 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
   const int CHY = TC * N;
 
   double pre[kDdPre];
-  double pre_nan = 0.0, pre_sum[4] = {0.0, 0.0, 0.0, 0.0};
+  double pre_nan = 0.0, pre_sum[4] = {0.0, 0.0, 0.0, 0.0}, pre_ymax = 0.0;
   auto load_chunk = [&](int c) {
     const size_t base = (size_t)c * CHY;
     const size_t lim = (size_t)T * N;
@@ -286,6 +389,7 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
     pre_nan = own ? prep[(size_t)tc * ldp + np + 2] : 0.0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) pre_sum[q] = own ? colsum[(size_t)tc * 4 + q] : 0.0;
+    pre_ymax = own ? colsum[(size_t)T * 4 + tc] : 0.0;
   };
   auto store_chunk = [&]() {
 #pragma unroll
@@ -297,6 +401,7 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
       s_nan[tid] = pre_nan;
       s_sum[2 * tid] = {pre_sum[0], pre_sum[1]};
       s_sum[2 * tid + 1] = {pre_sum[2], pre_sum[3]};
+      s_ymax[tid] = pre_ymax;
     }
   };
   if (nsteps > 0) {
@@ -313,12 +418,11 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
     const bool nan_col = s_nan[tt] != 0.0 || t >= my_data;
     if (act && nan_col) {
       // filter.jl:13-29: prediction only; F, F⁻¹, v stale → the loglik re-adds the last term
-      dd bf[M4], X[10];
+      dd bf[M4], X[M4][M4];
 #pragma unroll
       for (int i = 0; i < M4; ++i) bf[i] = beta[i];
-#pragma unroll
-      for (int q = 0; q < 10; ++q) X[q] = Pm[q];
-      dd_propagate(par, bf, X, false, beta, Pm);
+      gather_sym(Pc, X);
+      dd_propagate_q(par, qr, bf, X, false, xch, beta, Pc);
       if (acc) {
         sum_ld.add(dd_make(last_ld));
         sum_q.add(dd_make(last_q));
@@ -343,14 +447,38 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
       // basis (z2, z, z4) — z3 = z2 − z is recovered per step below.  The innovation sums are
       // recovered per step too: u = Z'y − Z'Z[:,1:3]β[1:3] and v'v = y'y − y'ŷ − ŷ'v, which in
       // dd keeps ≥ 80 of 106 bits where the FP64 kernel (yfm_tvl.hip) forms v per maturity.
+      // The sums of z, z2 and their products with each other and with y are σ-split accumulations
+      // (yfm_dd.hpp: dd_acc::add_sx): per step and lane, a tight bound on the terms over this lane's
+      // maturities (z = e^{−λm} ≤ e^{−λ m_min}, z2 = (1 − z)/(λm) ≤ min(1, 1/(λ m_min)), |y| ≤ the
+      // column's max) fixes the split constant.
+      const double lamh = lam.hi, rlh = rl.hi;
+      constexpr double kSlack = 1.0 + 0x1p-30;
+      const double Be = exp(-(lamh * l_minm)) * kSlack;
+      const double Bz2 = fmin(1.0, rlh * l_rminm) * kSlack;
+      const double By = s_ymax[tt] * l_n;
+#if YFM_DD_SPLIT_Z4
+      const double Bem = (lamh * l_minm >= 1.0 ? Be * l_minm : 0.36787944117144233 * rlh) * kSlack;
+      const double B4 = (Be * (fabs(k1.hi) + fabs(kr.hi) * l_rminm) + fabs(c2.hi) * Bem) * kSlack;
+      const double sg4 = split_const(l_n * B4), sg24 = split_const(l_n * Bz2 * B4);
+      const double sgz4 = split_const(l_n * Be * B4), sg44 = split_const(l_n * B4 * B4);
+      const double sy4 = split_const(By * B4);
+#endif
+      const double sg2 = split_const(l_n * Bz2), sgz = split_const(l_n * Be);
+      const double sg22 = split_const(l_n * Bz2 * Bz2), sg2z = split_const(l_n * Bz2 * Be);
+      const double sgzz = split_const(l_n * Be * Be);
+      const double sy2 = split_const(By * Bz2), syz = split_const(By * Be);
       dd_acc S2, Sz, S4, G22, G2z, G24, Gzz, Gz4, G44, Y2, Yz, Y4;
       auto accum = [&](int i, dd z) {
         const double m = s_m[i];
         const double y = col[i];
         const dd rm = s_rm[i];
-        const dd it = dd_mul_nn(rl, rm);                     // 1/τ
-        const dd z2 = dd_mul(dd_add_d(dd_neg(z), 1.0), it);  // (1 − z)/τ
+        const dd it = dd_mul_nn(rl, rm);  // 1/τ
+        // 1 − z exactly (Fast2Sum: 1 ≥ z.hi), then (1 − z)/τ
+        const double o1 = 1.0 - z.hi;
+        const dd ome = {o1, ((1.0 - o1) - z.hi) - z.lo};
+        const dd z2 = dd_mul_nn(ome, it);
         // ((β2+β3)(z/λ − z/(λ²m)) + β3·m·z)·(λ − 0.01) = z·t,  t = k1(1 − 1/τ) + c2·m
+        // (t left unnormalised: its products are formed to an absolute error of ~2^-104·|terms|)
         dd_acc ta;
         ta.hi = k1.hi;
         ta.lo = k1.lo;
@@ -360,27 +488,42 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
           p.lo = __builtin_fma(c2.lo, m, p.lo);
           ta.add(p);
         }
-        const dd z4 = dd_mul_nn(z, ta.value());
-        S2.add(z2);
-        Sz.add(z);
+        const dd z4 = dd_mul_nn(z, dd{ta.hi, ta.lo});
+        S2.add_sx(z2, sg2);
+        Sz.add_sx(z, sgz);
+        G22.add_prod_sx(z2, z2, sg22);
+        G2z.add_prod_sx(z2, z, sg2z);
+        Gzz.add_prod_sx(z, z, sgzz);
+        Y2.add_prod_d_sx(z2, y, sy2);
+        Yz.add_prod_d_sx(z, y, syz);
+#if YFM_DD_SPLIT_Z4
+        S4.add_sx(z4, sg4);
+        G24.add_prod_sx(z2, z4, sg24);
+        Gz4.add_prod_sx(z, z4, sgz4);
+        G44.add_prod_sx(z4, z4, sg44);
+        Y4.add_prod_d_sx(z4, y, sy4);
+#else
+        // the Jacobian-column sums keep TwoSum accumulation (|z4| has no tight per-lane bound:
+        // t = k1(1 − 1/τ) + c2·m cancels near λm = 1)
         S4.add(z4);
-        G22.add_prod(z2, z2);
-        G2z.add_prod(z2, z);
         G24.add_prod(z2, z4);
-        Gzz.add_prod(z, z);
         Gz4.add_prod(z, z4);
         G44.add_prod(z4, z4);
-        Y2.add_prod_d(z2, y);
-        Yz.add_prod_d(z, y);
         Y4.add_prod_d(z4, y);
+#endif
       };
       if (K > 0) {
         dd* w = s_w + grp * kDdWStride;
-        for (int q = j; q < K; q += L) w[q] = dd_exp(neg_rate(lam, s_gd[q]));
+        dd z = (j < N) ? dd_exp(neg_rate(lam, s_m[j])) : dd_make(0.0);
+        // a jump equal to some lane's first maturity (uniform grids: d = L·Δ = m_{L−1}) is that
+        // lane's start value — the same dd_exp of the same argument — so only the others cost an exp
+        for (int q = 0; q < K; ++q)
+          if (s_gsrc[q] == j) w[q] = z;
+        for (int q = j; q < K; q += L)
+          if (s_gsrc[q] < 0) w[q] = dd_exp(neg_rate(lam, s_gd[q]));
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        dd z = (j < N) ? dd_exp(neg_rate(lam, s_m[j])) : dd_make(0.0);
         for (int i = j; i < N; i += L) {
           const dd wn = w[s_gi[i]];
           accum(i, z);
@@ -439,41 +582,63 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
       const double dh = 1.0 + 1e-300 * G[3][3].hi;
       const bool upd = true;
 #else
-      // ---- capacitance solve: B̃ = σ²I + P G, W = B̃⁻¹P ----
-      dd A[M4][M4], W[M4][M4];
+      // ---- capacitance solve: B̃ = σ²I + P G, W = B̃⁻¹P, distributed over the quad:
+      // role qr forms row qr of B̃ (P symmetric: its row qr is the column it holds), every lane
+      // factorises the broadcast B̃ and solves for ONE right-hand side, column qr of P ----
+      dd A[M4][M4];
+      {
+        dd Ar[M4];
 #pragma unroll
-      for (int i = 0; i < M4; ++i)
-#pragma unroll
-        for (int c = 0; c < M4; ++c) {
+        for (int k = 0; k < M4; ++k) {
           dd_acc a;
-          if (i == c) a.add(sig2);
+          a.add(k == qr ? sig2 : dd_make(0.0));
 #pragma unroll
-          for (int l = 0; l < M4; ++l) a.add_prod(Pm[i <= l ? utri(i, l) : utri(l, i)], G[l][c]);
-          A[i][c] = a.value();
-          W[i][c] = Pm[i <= c ? utri(i, c) : utri(c, i)];
+          for (int l = 0; l < M4; ++l) a.add_prod(Pc[l], G[l][k]);
+          Ar[k] = a.value();
         }
+        gather_sym(Ar, A);
+      }
+      dd x[M4][1];
+#pragma unroll
+      for (int i = 0; i < M4; ++i) x[i][0] = Pc[i];
       dd det;
-      dd_gauss<M4, M4>(A, W, &det);
-      dd Ws[10];
+      dd_gauss<M4, 1>(A, x, &det);
+      // column qr of the symmetric part of W: (W[k][qr] + W[qr][k])/2 with W[qr][k] from role k (for
+      // k = qr the same value twice: exactly W[qr][qr]); dd_add commutes bitwise, so the roles agree
+      dd ws[M4];
 #pragma unroll
-      for (int i = 0; i < M4; ++i)
+      for (int k = 0; k < M4; ++k) xch[qr * M4 + k] = x[k][0];
+      wave_sync();
 #pragma unroll
-        for (int c = i; c < M4; ++c) Ws[utri(i, c)] = (i == c) ? W[i][i] : dd_ldexp(dd_add(W[i][c], W[c][i]), -1);
+      for (int k = 0; k < M4; ++k) ws[k] = dd_ldexp(dd_add(x[k][0], xch[k * M4 + qr]), -1);
+      wave_sync();
+      // K v = W u: component qr, then all four
+      dd kv[M4];
+      {
+        dd_acc a;
+#pragma unroll
+        for (int k = 0; k < M4; ++k) a.add_prod(ws[k], u[k]);
+        const dd kq = a.value();
+        kv[0] = quad_bcast<0>(kq);
+        kv[1] = quad_bcast<1>(kq);
+        kv[2] = quad_bcast<2>(kq);
+        kv[3] = quad_bcast<3>(kq);
+      }
       dd bf[M4];
       dd_acc uk;
 #pragma unroll
       for (int i = 0; i < M4; ++i) {
-        dd_acc a;
-#pragma unroll
-        for (int c = 0; c < M4; ++c) a.add_prod(Ws[i <= c ? utri(i, c) : utri(c, i)], u[c]);
-        const dd kv = a.value();
-        bf[i] = dd_add(beta[i], kv);
-        uk.add_prod(u[i], kv);
+        bf[i] = dd_add(beta[i], kv[i]);
+        uk.add_prod(u[i], kv[i]);
       }
       const double q = dd_to_double(dd_mul(dd_sub(vv, uk.value()), rsig2));
       const double dh = dd_to_double(det);
       const bool upd = dh != 0.0;  // inv(F) threw: return without updating (filter.jl:51-56)
-      if (upd) dd_propagate(par, bf, Ws, true, beta, Pm);
+      if (upd) {
+        dd Wf[M4][M4];
+        gather_sym(ws, Wf);
+        dd_propagate_q(par, qr, bf, Wf, true, xch, beta, Pc);
+      }
 #endif
       last_ld = upd ? log(fabs(dh)) : -__builtin_inf();
       last_q = upd ? q : __builtin_nan("");
@@ -486,6 +651,8 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
     }
     if constexpr (RECORD) {
       const int slot = t - max(0, my_steps - rec_len);
+      dd Pf[M4][M4];
+      gather_sym(Pc, Pf);  // every lane of the quad takes part in the exchange
       if (act && j == 0 && slot >= 0) {
         const size_t o = (size_t)b * (size_t)rec_len + slot;
 #pragma unroll
@@ -494,7 +661,7 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
 #pragma unroll
           for (int c = 0; c < M4; ++c)
 #pragma unroll
-            for (int i = 0; i < M4; ++i) rec_P[o * M4 * M4 + c * M4 + i] = dd_to_double(Pm[i <= c ? utri(i, c) : utri(c, i)]);
+            for (int i = 0; i < M4; ++i) rec_P[o * M4 * M4 + c * M4 + i] = dd_to_double(Pf[i][c]);
         }
       }
     }
@@ -536,7 +703,8 @@ template <int L>
 hipError_t launch_tvl_dd_l(const LaunchArgs& a, const double* rec_dd, const TvlGaps& g, int TC) {
   constexpr int GPB = kDdBlock / L;
   const int grid = (a.B + GPB - 1) / GPB;
-  const size_t shmem = sizeof(double) * (size_t)(3 * a.N + 5 * TC + TC * a.N + GPB * kDPar + 2 * GPB * kDdWStride) +
+  const size_t shmem = sizeof(double) * (size_t)(3 * a.N + 6 * TC + TC * a.N + GPB * kDPar + 2 * GPB * kDdWStride +
+                                               2 * GPB * M4 * M4) +
                        sizeof(int) * a.N;
   if (shmem > 160 * 1024) return hipErrorInvalidValue;  // gfx950: 160 KiB of LDS per workgroup
   auto* k = a.rec_beta ? &tvl_dd_loglik_kernel<L, true> : &tvl_dd_loglik_kernel<L, false>;
@@ -557,7 +725,7 @@ hipError_t launch_tvl_dd_l(const LaunchArgs& a, const double* rec_dd, const TvlG
 
 // per-candidate records, then the panel's dd column sums (4 doubles per column)
 size_t tvl_dd_scratch_bytes(int B, int T) {
-  return sizeof(double) * ((size_t)kDRecLen * (size_t)(B > 0 ? B : 1) + 4 * (size_t)(T > 0 ? T : 1));
+  return sizeof(double) * ((size_t)kDRecLen * (size_t)(B > 0 ? B : 1) + 5 * (size_t)(T > 0 ? T : 1));
 }
 
 int tvl_dd_lanes_for(int B, int N, int want) {
