@@ -64,15 +64,17 @@ enum yfm_status {
  * collapsed form, whose filter contracts, with ill-conditioned-loading candidates evaluated in
  * double-double — see yfm_last_batch_deferred)
  *   YFM_PREC_CERTIFIED (default)  TVλ in double-double (~106-bit) arithmetic.  A share of TVλ
- *       candidates amplify any FP64 rounding by 1e10..1e13 over T = 600 steps, so no FP64
+ *       candidates amplify any FP64 rounding by 1e10..1e20 over T = 600 steps, so no FP64
  *       evaluation — the reference's own dense path included — is then within 1e-9 of the
- *       exact value of filter.jl:12-80; this mode returns that value to the last FP64 bit
- *       (checked against a binary128 restatement).  ≈5.6× the cost of FP64.
- *   YFM_PREC_FP64  FP64 throughout, the fastest path — an UNVERIFIED mode, not a parity mode: on
- *       the rounding-amplifying candidates its result is as far from the exact value as FP64
- *       arithmetic leaves it, which can be further than the reference's own dense FP64 path
- *       (config-3 sample: up to 1.0e-2 relative from the exact value where the reference's path
- *       is at most 7.3e-4).  Use it for screening; use YFM_PREC_CERTIFIED for results. */
+ *       exact value of filter.jl:12-80; this mode returns that value to ~1e-13 (every candidate of
+ *       a 1,024-candidate config-3 sample within 5.5e-11 of a binary128 restatement, where the
+ *       reference's dense FP64 path is up to 1.1e-2 from it).  ≈4.6× the cost of FP64.
+ *   YFM_PREC_FP64  FP64 throughout, the fastest path — the reference's arithmetic class, not a
+ *       certified mode: on the rounding-amplifying candidates every FP64 result, the reference's
+ *       included, is rounding noise around the exact value (on the 1,024-candidate sample this mode
+ *       is closer to it than the reference's dense path at the median, p99 and max — 6.7e-3 vs
+ *       1.1e-2 — but either can be the closer one on a given candidate).  Use YFM_PREC_CERTIFIED for
+ *       results that must not depend on rounding. */
 enum yfm_precision { YFM_PREC_CERTIFIED = 0, YFM_PREC_FP64 = 1 };
 
 /* Library/ABI introspection. */
