@@ -127,9 +127,10 @@ struct dd_acc {
     hi += q;
     lo += (x.hi - q) + x.lo;
   }
-  // += a·b: a.hi·b.hi − q to one rounding (|·| ≤ ulp(σ)), plus the cross terms
+  // += a·b: q = fl(σ + a.hi·b.hi) − σ (one FMA: the exact product rounded to a multiple of ulp(σ)),
+  // a.hi·b.hi − q to one rounding (|·| ≤ ulp(σ)), plus the cross terms
   __device__ __forceinline__ void add_prod_sx(dd a, dd b, double sg) {
-    const double q = (sg + a.hi * b.hi) - sg;
+    const double q = __builtin_fma(a.hi, b.hi, sg) - sg;
     hi += q;
     lo += __builtin_fma(a.hi, b.hi, -q);
     lo = __builtin_fma(a.hi, b.lo, lo);
@@ -137,7 +138,7 @@ struct dd_acc {
   }
   // += a·d (d a double)
   __device__ __forceinline__ void add_prod_d_sx(dd a, double d, double sg) {
-    const double q = (sg + a.hi * d) - sg;
+    const double q = __builtin_fma(a.hi, d, sg) - sg;
     hi += q;
     lo += __builtin_fma(a.hi, d, -q);
     lo = __builtin_fma(a.lo, d, lo);

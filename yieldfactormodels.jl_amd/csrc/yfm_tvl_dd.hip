@@ -340,10 +340,11 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
   for (int q = j; q < kDPar; q += L) par[q] = r[q];
   __syncthreads();
   // this lane's maturities i ≡ j (mod L): count and smallest maturity (bounds of the σ-split sums)
-  double l_n = 0.0, l_minm = __builtin_inf();
+  double l_n = 0.0, l_minm = __builtin_inf(), l_maxm = 0.0;
   for (int i = j; i < N; i += L) {
     l_n += 1.0;
     l_minm = fmin(l_minm, s_m[i]);
+    l_maxm = fmax(l_maxm, s_m[i]);
   }
   const double l_rminm = 1.0 / l_minm;
   const int my_steps = horizon > 0 ? nobs + horizon : nobs - 1;
@@ -456,6 +457,10 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
       const double Be = exp(-(lamh * l_minm)) * kSlack;
       const double Bz2 = fmin(1.0, rlh * l_rminm) * kSlack;
       const double By = s_ymax[tt] * l_n;
+      // t = k1 − kr/m + c2·m per maturity, σ-split with the bound of its three terms (k1's split once per step)
+      const double sgt = split_const((fabs(k1.hi) + fabs(kr.hi) * l_rminm + fabs(c2.hi) * l_maxm) * kSlack);
+      const double qk1 = (sgt + k1.hi) - sgt;
+      const double rk1 = (k1.hi - qk1) + k1.lo;
 #if YFM_DD_SPLIT_Z4
       const double Bem = (lamh * l_minm >= 1.0 ? Be * l_minm : 0.36787944117144233 * rlh) * kSlack;
       const double B4 = (Be * (fabs(k1.hi) + fabs(kr.hi) * l_rminm) + fabs(c2.hi) * Bem) * kSlack;
@@ -479,16 +484,16 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
         const dd z2 = dd_mul_nn(ome, it);
         // ((β2+β3)(z/λ − z/(λ²m)) + β3·m·z)·(λ − 0.01) = z·t,  t = k1(1 − 1/τ) + c2·m
         // (t left unnormalised: its products are formed to an absolute error of ~2^-104·|terms|)
-        dd_acc ta;
-        ta.hi = k1.hi;
-        ta.lo = k1.lo;
-        ta.add(dd_mul_nn(dd_neg(kr), rm));
+        dd ta;
         {
-          dd p = two_prod(c2.hi, m);
-          p.lo = __builtin_fma(c2.lo, m, p.lo);
-          ta.add(p);
+          const double q1 = __builtin_fma(-kr.hi, rm.hi, sgt) - sgt;
+          const double l1 = __builtin_fma(-kr.hi, rm.lo, __builtin_fma(-kr.lo, rm.hi, __builtin_fma(-kr.hi, rm.hi, -q1)));
+          const double q2 = __builtin_fma(c2.hi, m, sgt) - sgt;
+          const double l2 = __builtin_fma(c2.lo, m, __builtin_fma(c2.hi, m, -q2));
+          ta.hi = (qk1 + q1) + q2;  // exact: multiples of ulp(σ) below σ
+          ta.lo = (rk1 + l1) + l2;
         }
-        const dd z4 = dd_mul_nn(z, dd{ta.hi, ta.lo});
+        const dd z4 = dd_mul_nn(z, ta);
         S2.add_sx(z2, sg2);
         Sz.add_sx(z, sgz);
         G22.add_prod_sx(z2, z2, sg22);
