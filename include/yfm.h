@@ -67,8 +67,8 @@ enum yfm_status {
  *       candidates amplify any FP64 rounding by 1e10..1e20 over T = 600 steps, so no FP64
  *       evaluation — the reference's own dense path included — is then within 1e-9 of the
  *       exact value of filter.jl:12-80; this mode returns that value to ~1e-13 (every candidate of
- *       a 1,024-candidate config-3 sample within 5.5e-11 of a binary128 restatement, where the
- *       reference's dense FP64 path is up to 1.1e-2 from it).  ≈4.6× the cost of FP64.
+ *       a 1,024-candidate config-3 sample within 1.6e-10 of a binary128 restatement, where the
+ *       reference's dense FP64 path is up to 1.1e-2 from it).  ≈4× the cost of FP64.
  *   YFM_PREC_FP64  FP64 throughout, the fastest path — the reference's arithmetic class, not a
  *       certified mode: on the rounding-amplifying candidates every FP64 result, the reference's
  *       included, is rounding noise around the exact value (on the 1,024-candidate sample this mode
