@@ -69,6 +69,17 @@ def collapsed_update_flops(M: int) -> float:
     return f + 3
 
 
+def steady_update_flops(M: int) -> float:
+    """FP64 operations of one steady-state step of the DNS kernel (frozen covariance, yfm_fixedz.hpp
+    FixedZFilter::steady_step): ĉ, the residual, c = ĉ − β, x = S⁻¹c with the cached LDLᵀ factors,
+    c'x, q, β_{t|t} = β + P x, β ← δ + Φβ and the loglik accumulation — the covariance half is not run."""
+    nz = M - 1
+    f = nz + 2 * M * nz + 2 * nz + 1 + M      # z̃/σ², ĉ, residual, ĉ₀ += ȳ, c = ĉ − β
+    f += 2 * M * (M - 1) + M + 2 * M + 2      # x = S⁻¹c, c'x, q
+    f += 2 * M * M + 2 * M * M                # β_{t|t} = β + P x, β ← δ + Φβ
+    return f + 3
+
+
 def alg_flops_step(kind: int, N: int, M: int) -> float:
     """Algorithmic FP64 flops of one update step of the formulation this build runs:
     fixed loadings (DNS, GNS5): the collapsed form — z̃ = Z'ỹ (2N(M−1)) plus the M×M update;
@@ -321,18 +332,27 @@ def pmc_traffic(kernel_substr: str, evals: int):
     return None, None
 
 
-DOMINANT = {KIND_DNS: "fixedz_loglik_kernel<30, 3, 1, false>", KIND_GNS: "fixedz_loglik_kernel<30, 5, 2, false>",
+DOMINANT = {KIND_DNS: "fixedz_loglik_kernel<30, 3, 1, false, true>", KIND_GNS: "fixedz_loglik_kernel<30, 5, 2, false, false>",
+            (KIND_DNS, "full"): "fixedz_loglik_kernel<30, 3, 1, false, false>",
             (KIND_TVL, "fp64"): "tvl_loglik_kernel", (KIND_TVL, "certified"): "tvl_dd_loglik_kernel"}
 
 
-def roofline(kind, prec, N, M, T, T_use, B, P, kernel_ms):
+def roofline(kind, prec, N, M, T, T_use, B, P, kernel_ms, steady_lane_steps=0):
     """The dominant kernel against the FP64 VALU roofline: achieved = algorithmic flops of the
-    formulation it runs (alg_flops) for this GPU's batch ÷ HIP-event time per launch."""
+    formulation it runs (alg_flops) for this GPU's batch ÷ HIP-event time per launch.  Filter steps
+    run in the DNS kernel's frozen-covariance steady state (`steady_lane_steps`, measured by the
+    kernel: yfm_last_batch_steady × 64) count the steady step's flops instead of the full update's."""
     Tb = T_use if T_use is not None else np.full(B, T)
     f_rank = float(np.sum(alg_flops(kind, N, M, Tb)))
+    f_rank -= steady_lane_steps * (collapsed_update_flops(M) - steady_update_flops(M))
     f_survey = float(np.sum(alg_flops(kind, N, M, Tb, survey_flops_step)))
     achieved = f_rank / (kernel_ms * 1e-3) / 1e12
-    name = DOMINANT[(kind, prec)] if kind == KIND_TVL else DOMINANT[kind]
+    if kind == KIND_TVL:
+        name = DOMINANT[(kind, prec)]
+    elif kind == KIND_DNS and os.environ.get("YFM_DNS_STEADY", "1").startswith("0"):
+        name = DOMINANT[(kind, "full")]  # the full-recursion instantiation
+    else:
+        name = DOMINANT[kind]
     traffic, traffic_src = pmc_traffic(name, B)
     exe = pmc_executed_flops(name, B)
     steps = float(np.sum(Tb - 1))
@@ -343,7 +363,9 @@ def roofline(kind, prec, N, M, T, T_use, B, P, kernel_ms):
             "algorithmic_bytes": B * (P + 1) * 8 + T * (N + 4) * 8, "kernel": name, "kernel_ms": kernel_ms,
             "flops_per_eval": f_rank / max(B, 1),
             "flop_model": ("SURVEY §8d capacitance form (62N + 939 per step)" if kind == KIND_TVL else
-                           "collapsed form: 2N(M−1) for Z'ỹ + the M×M update (bench.py collapsed_update_flops)"),
+                           "collapsed form: 2N(M−1) for Z'ỹ + the M×M update (bench.py collapsed_update_flops); "
+                           "frozen-covariance steady steps: 2N(M−1) + the mean update (steady_update_flops)"),
+            "steady_lane_steps": int(steady_lane_steps),
             "survey_equiv_tflops": f_survey / (kernel_ms * 1e-3) / 1e12,
             "executed_tflops": exe_tf, "executed_frac": exe_tf / FP64_PEAK_TFLOPS if exe_tf else None,
             "executed_frac_vs_measured_peak": exe_tf / FP64_MEASURED_TFLOPS if exe_tf else None,
@@ -501,8 +523,31 @@ def main():
     best_main = best[0]
     ms_per_step = 1e3 * wall / args.steps
     value = w.global_batch / (wall / args.steps)
-    roof = roofline(kind, args.precision, N, M, T, w.T_use, B, P, kernel_ms)
+    steady_ws = eng.last_steady() if kind == KIND_DNS else 0  # frozen-covariance wave-steps of the last launch
+    roof = roofline(kind, args.precision, N, M, T, w.T_use, B, P, kernel_ms, steady_lane_steps=64 * steady_ws)
     out_host = d_out.cpu().numpy()
+    # DNS: the same workload with the full covariance recursion every step (YFM_DNS_STEADY=0), beside the
+    # default — the steady state must not change a loglik by more than rounding (tests/test_gpu_steady.py)
+    steady = None
+    if kind == KIND_DNS:
+        Tb = w.T_use if w.T_use is not None else np.full(B, T)
+        os.environ["YFM_DNS_STEADY"] = "0"
+        try:
+            wall_full, kms_full = timed(args.steps, max(1, args.warmup // 2))
+            full_host = d_out.cpu().numpy()
+        finally:
+            os.environ.pop("YFM_DNS_STEADY", None)
+        fin = np.isfinite(full_host)
+        dr = np.abs(out_host[fin] - full_host[fin]) / np.abs(full_host[fin])
+        steady = {"steady_lane_steps": 64 * steady_ws, "frac_of_filter_steps": 64 * steady_ws / float(np.sum(Tb - 1)),
+                  "full_recursion_evals_per_s": w.global_batch / (wall_full / args.steps),
+                  "full_recursion_kernel_ms": kms_full,
+                  "vs_full_recursion_max_rel": float(dr.max()) if dr.size else 0.0,
+                  "pattern_match": bool(np.array_equal(np.isfinite(out_host), fin)),
+                  "note": "the covariance recursion of filter.jl:158-176 is data-independent for fixed loadings; each "
+                          "candidate freezes P once its change per step is at the rounding level (a step set by its "
+                          "own θ), a wave whose candidates are all frozen runs the mean update only "
+                          "(DESIGN.md §3.1; YFM_DNS_STEADY=0 disables it)"}
     n_neginf, n_nan = int(np.isneginf(out_host).sum()), int(np.isnan(out_host).sum())
     n_deferred = eng.last_deferred()  # candidates of the last timed batch on the double-double path
 
@@ -585,6 +630,8 @@ def main():
         }
         if fp64_mode:
             line["fp64_mode"] = fp64_mode
+        if steady:
+            line["steady_state"] = steady
         if best_main is not None:
             line["best_candidate"] = {"loglik": float(best_main[0].item()), "index": int(best_main[1].item())}
         print(json.dumps(line), flush=True)

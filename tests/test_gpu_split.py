@@ -17,13 +17,16 @@ pytestmark = pytest.mark.gpu
 
 
 def both(fn):
-    """(one filter per lane, two-wave split) results of fn()."""
-    a = fn()
-    os.environ["YFM_DNS_SPLIT"] = "1"
+    """(one filter per lane, two-wave split) results of fn().  The per-lane kernel runs without its
+    frozen-covariance steady state (YFM_DNS_STEADY=0), which the split kernel does not implement."""
+    os.environ["YFM_DNS_STEADY"] = "0"
     try:
+        a = fn()
+        os.environ["YFM_DNS_SPLIT"] = "1"
         b = fn()
     finally:
         os.environ.pop("YFM_DNS_SPLIT", None)
+        os.environ.pop("YFM_DNS_STEADY", None)
     return a, b
 
 

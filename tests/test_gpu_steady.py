@@ -1,0 +1,100 @@
+"""The frozen-covariance steady state of the DNS loglik kernel (FixedZFilter).
+
+With the loadings fixed, the covariance recursion of filter.jl:158-176 does not depend on the data and
+converges to the Riccati fixed point; each lane freezes its P once the change is at the rounding level
+(and the estimated remaining drift below 2^-50), and a wave whose lanes are all frozen runs the mean
+update only.  Checked here:
+* against the full recursion (YFM_DNS_STEADY=0): every loglik within 1e-12 relative (config-2 batch,
+  ragged windows with NaN columns, near-unit-root Φ);
+* determinism: a candidate's loglik does not depend on its batch (the freeze step is a function of its
+  own θ) — the same θ in a permuted and a sub-sampled batch gives the same bits;
+* factor-1 parity against the dense oracle / binary128 truth on the config-2 sample.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+from oracle.truth import loglik_oracle, loglik_truth
+from test_gpu_parity import assert_parity
+from yfm_amd import KIND_DNS
+from yfm_amd import synthetic as S
+
+pytestmark = pytest.mark.gpu
+
+
+def full(fn):
+    os.environ["YFM_DNS_STEADY"] = "0"
+    try:
+        return fn()
+    finally:
+        os.environ.pop("YFM_DNS_STEADY", None)
+
+
+def rel(a, b):
+    fin = np.isfinite(b)
+    assert np.array_equal(np.isfinite(a), fin) and np.array_equal(np.isnan(a), np.isnan(b))
+    return np.abs(a[fin] - b[fin]) / np.maximum(np.abs(b[fin]), 1e-300)
+
+
+@pytest.fixture(scope="module")
+def config2(engine):
+    Y = S.simulate_panel(KIND_DNS, 600)
+    mats = S.maturities_30()
+    engine.set_panel(Y, mats)
+    return Y, mats, S.theta_batch(KIND_DNS, 65536)
+
+
+def test_steady_vs_full_recursion_config2(engine, config2):
+    Y, mats, Th = config2
+    engine.set_panel(Y, mats)
+    got = engine.loglik(KIND_DNS, Th)
+    frac = 64 * engine.last_steady() / (Th.shape[1] * 599.0)
+    ref = full(lambda: engine.loglik(KIND_DNS, Th))
+    assert engine.last_steady() == 0  # the full-recursion instantiation
+    print("steady share of the filter steps: %.3f" % frac)
+    assert frac > 0.9  # every wave of the config-2 batch freezes within its first blocks
+    e = rel(got, ref)
+    print("config 2: steady vs full recursion max rel %.3e, bitwise-equal fraction %.4f"
+          % (e.max(), np.mean(got[np.isfinite(ref)] == ref[np.isfinite(ref)])))
+    assert e.max() <= 1e-12
+
+
+def test_steady_is_batch_independent(engine, config2):
+    Y, mats, Th = config2
+    engine.set_panel(Y, mats)
+    B = 8192
+    sub = np.asfortranarray(Th[:, :B])
+    a = engine.loglik(KIND_DNS, sub)
+    perm = np.random.default_rng(5).permutation(B)
+    b = engine.loglik(KIND_DNS, np.asfortranarray(sub[:, perm]))
+    np.testing.assert_array_equal(a[perm], b)
+    c = engine.loglik(KIND_DNS, np.asfortranarray(sub[:, 3::7]))
+    np.testing.assert_array_equal(a[3::7], c)
+
+
+def test_steady_parity_config2_sample(engine, config2):
+    Y, mats, Th = config2
+    engine.set_panel(Y, mats)
+    sub = np.asfortranarray(Th[:, :256])
+    got = engine.loglik(KIND_DNS, sub)
+    table = assert_parity(got, loglik_oracle(KIND_DNS, Y, mats, sub), loglik_truth(KIND_DNS, Y, mats, sub))
+    assert table["failing"] == 0
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_steady_windows_nan_unit_root(engine, seed):
+    rng = np.random.default_rng(seed)
+    mats = S.maturities_30()
+    Y = S.simulate_panel(KIND_DNS, 400, maturities=mats).copy(order="F")
+    Y[:, [50, 51, 200, 333]] = np.nan  # prediction-only steps thaw the frozen lanes
+    engine.set_panel(Y, mats)
+    Th = S.theta_batch(KIND_DNS, 4096, seed=100 + seed)
+    Th[-9:, :64] = 0.0  # Φ = 0 off the diagonal …
+    Th[-9, :64] = Th[-5, :64] = Th[-1, :64] = 8.0  # … and φ_ii = 2/(1+e^-8)−1 ≈ 0.9993: near-unit-root
+    tu = rng.integers(2, 401, Th.shape[1]).astype(np.int32)
+    got = engine.loglik(KIND_DNS, Th, T_use=tu)
+    ref = full(lambda: engine.loglik(KIND_DNS, Th, T_use=tu))
+    assert rel(got, ref).max() <= 1e-12

@@ -72,7 +72,7 @@ struct DevBuf {
 // Per-launch device work buffers.  A context owns one; the estimation driver adds one per extra
 // concurrent stream (launches in flight on different streams must not share them).
 struct yfm::Workspace {
-  DevBuf flags;       // 2 banks × 4 unsigned int: n_init_throw, n_neg_inf, deferral list length, n_deferred
+  DevBuf flags;       // 2 banks × kFlagsPerBank unsigned int: n_init_throw, n_neg_inf, deferral list length, n_deferred, steady wave-steps
   int bank = 0;       // the bank of the last launch (the other one is zeroed by that launch's first kernel)
   DevBuf scratch;     // per-candidate work records (TVλ / GNS5 / two-wave DNS init)
   DevBuf scratch_dd;  // TVλ double-double records (YFM_PREC_CERTIFIED)
@@ -90,7 +90,7 @@ struct yfm_ctx {
   DevBuf panel, mats, raw;
   // staging for host-pointer calls
   DevBuf theta, out, tuse, rec_beta, rec_P;
-  DevBuf flags;  // 2 banks × 4 unsigned int: n_init_throw, n_neg_inf, deferral list length, n_deferred
+  DevBuf flags;  // 2 banks × kFlagsPerBank unsigned int: n_init_throw, n_neg_inf, deferral list length, n_deferred, steady wave-steps
   int bank = 0;  // the bank of the last launch (the other one is zeroed by that launch's first kernel)
   DevBuf scratch;  // per-candidate work records (TVλ init)
   DevBuf scratch_dd;  // TVλ double-double records (YFM_PREC_CERTIFIED)
@@ -211,12 +211,12 @@ int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int 
   unsigned int* flags_next = nullptr;
   if (reset_flags) {
     w_bank ^= 1;
-    flags_next = fb + 4 * (w_bank ^ 1);
+    flags_next = fb + yfm::kFlagsPerBank * (w_bank ^ 1);
   } else {
-    YFM_HIP_CHECK(hipMemsetAsync(fb + 4 * w_bank + 2, 0, sizeof(unsigned int), s));
+    YFM_HIP_CHECK(hipMemsetAsync(fb + yfm::kFlagsPerBank * w_bank + 2, 0, sizeof(unsigned int), s));
   }
   if (B == 0) {  // no kernel runs: zero both banks here
-    YFM_HIP_CHECK(hipMemsetAsync(fb, 0, 8 * sizeof(unsigned int), s));
+    YFM_HIP_CHECK(hipMemsetAsync(fb, 0, 2 * yfm::kFlagsPerBank * sizeof(unsigned int), s));
     return YFM_OK;
   }
   yfm::LaunchArgs a;
@@ -233,7 +233,7 @@ int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int 
   a.mats = static_cast<const double*>(ctx->mats.p);
   a.T_use = d_T_use;
   a.out = d_out;
-  a.flags = fb + 4 * w_bank;
+  a.flags = fb + yfm::kFlagsPerBank * w_bank;
   a.flags_next = flags_next;
   a.rec_beta = d_rb;
   a.rec_P = d_rP;
@@ -387,12 +387,12 @@ yfm_ctx* yfm_create(int hip_device) {
   yfm_ctx* ctx = new yfm_ctx();
   ctx->device = hip_device;
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
-      ctx->flags.ensure(8 * sizeof(unsigned int)) != hipSuccess) {
+      ctx->flags.ensure(2 * yfm::kFlagsPerBank * sizeof(unsigned int)) != hipSuccess) {
     set_error(YFM_EHIP, "context allocation failed on device %d", hip_device);
     yfm_destroy(ctx);
     return nullptr;
   }
-  (void)hipMemset(ctx->flags.p, 0, 8 * sizeof(unsigned int));
+  (void)hipMemset(ctx->flags.p, 0, 2 * yfm::kFlagsPerBank * sizeof(unsigned int));
   return ctx;
 }
 
@@ -582,7 +582,7 @@ int yfm_filter_states(yfm_ctx* ctx, int model_kind, int param_space, const doubl
 int yfm_last_batch_flags(yfm_ctx* ctx, long long* n_init_throw, long long* n_neg_inf) {
   if (int r = check_ctx(ctx)) return r;
   unsigned int h[2] = {0, 0};
-  YFM_HIP_CHECK(hipMemcpy(h, static_cast<unsigned int*>(ctx->flags.p) + 4 * ctx->bank, sizeof(h), hipMemcpyDeviceToHost));
+  YFM_HIP_CHECK(hipMemcpy(h, static_cast<unsigned int*>(ctx->flags.p) + yfm::kFlagsPerBank * ctx->bank, sizeof(h), hipMemcpyDeviceToHost));
   if (n_init_throw) *n_init_throw = h[0];
   if (n_neg_inf) *n_neg_inf = h[1];
   return YFM_OK;
@@ -591,8 +591,17 @@ int yfm_last_batch_flags(yfm_ctx* ctx, long long* n_init_throw, long long* n_neg
 int yfm_last_batch_deferred(yfm_ctx* ctx, long long* n_deferred) {
   if (int r = check_ctx(ctx)) return r;
   unsigned int h[4] = {0, 0, 0, 0};
-  YFM_HIP_CHECK(hipMemcpy(h, static_cast<unsigned int*>(ctx->flags.p) + 4 * ctx->bank, sizeof(h), hipMemcpyDeviceToHost));
+  YFM_HIP_CHECK(hipMemcpy(h, static_cast<unsigned int*>(ctx->flags.p) + yfm::kFlagsPerBank * ctx->bank, sizeof(h), hipMemcpyDeviceToHost));
   if (n_deferred) *n_deferred = h[3];
+  return YFM_OK;
+}
+
+int yfm_last_batch_steady(yfm_ctx* ctx, long long* steady_wave_steps) {
+  if (int r = check_ctx(ctx)) return r;
+  unsigned int h[5] = {0, 0, 0, 0, 0};
+  YFM_HIP_CHECK(hipMemcpy(h, static_cast<unsigned int*>(ctx->flags.p) + yfm::kFlagsPerBank * ctx->bank, sizeof(h),
+                          hipMemcpyDeviceToHost));
+  if (steady_wave_steps) *steady_wave_steps = h[4];
   return YFM_OK;
 }
 
@@ -691,7 +700,7 @@ int yfm_loss_array(yfm_ctx* ctx, int model_kind, int param_space, const double* 
   }
   const int rec_len = pv.T - 1;
   if (int r = run_trajectory(ctx, model_kind, param_space, d_th, P, B, d_tu, 0, rec_len, &pv)) return r;
-  unsigned int* cur = static_cast<unsigned int*>(ctx->flags.p) + 4 * ctx->bank;
+  unsigned int* cur = static_cast<unsigned int*>(ctx->flags.p) + yfm::kFlagsPerBank * ctx->bank;
   YFM_HIP_CHECK(hipMemsetAsync(cur, 0, 2 * sizeof(unsigned int), ctx->stream));
   YFM_HIP_CHECK(ctx->rec_P.ensure(sizeof(double) * (size_t)T1 * B));
   yfm::PredictArgs a = predict_args(ctx, model_kind, d_th, P, B, d_tu, 1, rec_len);
@@ -709,8 +718,8 @@ namespace yfm {
 
 Workspace* workspace_create() {
   auto* w = new Workspace;
-  if (w->flags.ensure(8 * sizeof(unsigned int)) != hipSuccess ||
-      hipMemset(w->flags.p, 0, 8 * sizeof(unsigned int)) != hipSuccess) {
+  if (w->flags.ensure(2 * yfm::kFlagsPerBank * sizeof(unsigned int)) != hipSuccess ||
+      hipMemset(w->flags.p, 0, 2 * yfm::kFlagsPerBank * sizeof(unsigned int)) != hipSuccess) {
     delete w;
     return nullptr;
   }

@@ -15,6 +15,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "yfm_flags.hpp"
+
 namespace yfm {
 
 constexpr double kLog2Pi = 1.8378770664093454835606594728112;  // log(2π)

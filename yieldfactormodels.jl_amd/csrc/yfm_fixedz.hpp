@@ -163,7 +163,41 @@ __device__ __forceinline__ void collapsed_update(const double (&zt)[M - 1], doub
 // benchmark lane is deferred while the error of every collapsed lane stays ≲ 3e-11.
 constexpr double kCollapsedKappa = 1e6;
 
-template <int M, int LEAD, bool RECORD>
+// P ← Φ P_{t|t} Φ' + Q as propagate_cov_f (bitwise), except that a frozen lane keeps its P; returns the
+// largest change of an entry and the largest new entry (the freeze test of FixedZFilter)
+template <int M, int LEAD>
+__device__ __forceinline__ void propagate_cov_freeze(const Params<M, LEAD>& p, const double (&Pf)[M][M],
+                                                     double (&Pm)[M][M], bool frozen, double& dmax, double& nmax) {
+  double A[M][M];
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      double a = 0.0;
+#pragma unroll
+      for (int l = 0; l < M; ++l) a = fma(p.Phi[i][l], (l <= j) ? Pf[l][j] : Pf[j][l], a);
+      A[i][j] = a;
+    }
+  }
+  dmax = 0.0;
+  nmax = 0.0;
+#pragma unroll
+  for (int j = 0; j < M; ++j) {
+#pragma unroll
+    for (int i = 0; i <= j; ++i) {
+      double t = p.Q[i][j];
+#pragma unroll
+      for (int l = 0; l < M; ++l) t = fma(A[i][l], p.Phi[j][l], t);
+      dmax = fmax(dmax, fabs(t - Pm[i][j]));
+      nmax = fmax(nmax, fabs(t));
+      const double v = frozen ? Pm[i][j] : t;
+      Pm[i][j] = v;
+      Pm[j][i] = v;
+    }
+  }
+}
+
+template <int M, int LEAD, bool RECORD, bool STEADY = false>
 struct FixedZFilter {
   Params<M, LEAD> p;
   double sigma2, rsig2;
@@ -176,6 +210,61 @@ struct FixedZFilter {
   double sumq = 0.0;
   bool neg = false;
   double last_det = 0.0, last_q = 0.0;  // fresh model: F = 0, F⁻¹ = 0, v = 0 (kalmanbasemodel.jl:65-67)
+
+  // ---- frozen covariance (STEADY: loglik mode of the per-lane kernel) ----
+  // With Z fixed the covariance recursion P ↦ Φ P(P + R)⁻¹R Φ' + Q does not depend on the data and
+  // converges geometrically to the Riccati fixed point.  A lane freezes its P after the data step at
+  // which the relative change of P is ≤ 2^-46 and the remaining geometric drift, estimated from the
+  // ratio ρ of successive changes, is ≤ 2^-50 (d·ρ/(1 − ρ)); a frozen lane keeps P (and so S = P + R
+  // and its factors) for every later data step, until a prediction-only step (a NaN column) moves P.
+  // The freeze step depends on the lane's θ alone, so its loglik does not depend on the batch.  Once
+  // EVERY lane of a wave is frozen the wave runs the mean update only, with the factors of S cached —
+  // bitwise the full step's values for a frozen lane (the same S, factorised by the same code).
+  bool steady_ok = false;    // the runtime switch (YFM_DNS_STEADY, default on)
+  bool frozen = false;
+  double prevd = __builtin_inf();
+  bool wave_frozen = false;  // wave-uniform
+  LDLT<M> fs;                // factors of S = P + R at the frozen P (valid while wave_frozen)
+  double dets = 0.0;
+
+  // the freeze test after a data step that moved P by (dmax, nmax)
+  __device__ __forceinline__ void freeze_test(double dmax, double nmax) {
+    const double d = dmax / nmax;
+    const double rho = d / prevd;
+    const bool ok = (d <= 0x1p-46) && (rho < 0.999) && (d * rho <= 0x1p-50 * (1.0 - rho));
+    prevd = frozen ? prevd : d;
+    frozen = frozen || (ok && steady_ok);
+  }
+  // a prediction-only step moves P: every lane thaws
+  __device__ __forceinline__ void thaw() {
+    frozen = false;
+    prevd = __builtin_inf();
+    wave_frozen = false;
+  }
+  // wave vote (every lane of the wave calls this at the same point): `part` = the lane's result counts
+  __device__ __forceinline__ void wave_freeze(bool part) {
+    if (wave_frozen) return;
+    if (__all(frozen || !part)) {
+      double S[M][M];
+#pragma unroll
+      for (int i = 0; i < M; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j) S[i][j] = Pm[i][j] + R[i][j];
+      dets = fs.factor(S);
+      wave_frozen = true;
+    }
+  }
+  // one data step of a frozen wave: the mean update of collapsed_update with the cached factors
+  __device__ __forceinline__ void steady_step(const double (&zc)[M - 1], double2 yb_c) {
+    double bf[M], q;
+    collapsed_mean<M>(zc, yb_c.x, yb_c.y, R, rsig2, beta, Pm, fs, bf, q);
+    propagate_mean_f<M>([&](int i, int j) { return p.Phi[i][j]; }, p.delta, bf, beta);
+    last_det = dets;
+    last_q = q;
+    ld.mul(dets);
+    sumq += q;
+    neg = neg || (dets < 0.0);
+  }
 
   // G = Z'Z → R, log det G, collapsed or deferred; then initialize_filter.
   // do_init = false: the caller loads the initial state itself (fixedz_init_kernel's record)
@@ -226,7 +315,14 @@ struct FixedZFilter {
       double bf[M], Pf[M][M], det, q;
       collapsed_update<M>(zc, yb_c.x, yb_c.y, R, rsig2, beta, Pm, bf, Pf, det, q);
       // (a singular F at t ≥ 2 makes the loglik −Inf whatever the state; trajectories skip the update)
-      if (!RECORD || det != 0.0) propagate_state<M, LEAD>(p, bf, Pf, beta, Pm);
+      if constexpr (STEADY) {
+        propagate_mean_f<M>([&](int i, int j) { return p.Phi[i][j]; }, p.delta, bf, beta);
+        double dmax, nmax;
+        propagate_cov_freeze<M, LEAD>(p, Pf, Pm, frozen, dmax, nmax);
+        freeze_test(dmax, nmax);
+      } else if (!RECORD || det != 0.0) {
+        propagate_state<M, LEAD>(p, bf, Pf, beta, Pm);
+      }
       last_det = det;
       last_q = q;
       ld.mul(det);
@@ -249,6 +345,7 @@ struct FixedZFilter {
 #pragma unroll
       for (int i = 0; i < M; ++i) bf[i] = beta[i];
       propagate_state<M, LEAD>(p, bf, Pf, beta, Pm);
+      if constexpr (STEADY) thaw();
       if (acc) {
         ld.mul(last_det);
         sumq += last_q;
@@ -261,7 +358,16 @@ struct FixedZFilter {
     double Pf[M][M];
     collapsed_update<M>(zc, yb_c.x, yb_c.y, R, rsig2, beta, Pm, bf, Pf, det, q);
     const bool upd = det != 0.0;  // inv(F) threw: return without the update (filter.jl:151-154)
-    if (upd) propagate_state<M, LEAD>(p, bf, Pf, beta, Pm);
+    if constexpr (STEADY) {
+      if (upd) {
+        propagate_mean_f<M>([&](int i, int j) { return p.Phi[i][j]; }, p.delta, bf, beta);
+        double dmax, nmax;
+        propagate_cov_freeze<M, LEAD>(p, Pf, Pm, frozen, dmax, nmax);
+        freeze_test(dmax, nmax);
+      }
+    } else if (upd) {
+      propagate_state<M, LEAD>(p, bf, Pf, beta, Pm);
+    }
     last_det = det;
     last_q = upd ? q : __builtin_nan("");
     if (acc) {

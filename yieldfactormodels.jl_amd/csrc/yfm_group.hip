@@ -38,7 +38,7 @@ __global__ __launch_bounds__(kGBlock, 2) void fixedz_group_kernel(
     int T, int N, int TC, const double* __restrict__ mats, const int* __restrict__ T_use, double* __restrict__ out,
     unsigned int* __restrict__ flags, double* __restrict__ rec_beta, double* __restrict__ rec_P, int horizon,
     int rec_len, int* __restrict__ defer_list, int* __restrict__ defer_count, unsigned int* __restrict__ flags_next) {
-  if (flags_next && blockIdx.x == 0 && threadIdx.x < 4) flags_next[threadIdx.x] = 0u;  // the next launch's counters
+  if (flags_next && blockIdx.x == 0 && threadIdx.x < kFlagsPerBank) flags_next[threadIdx.x] = 0u;  // the next launch's counters
   constexpr int NZ = M - 1;
   constexpr int GPB = kGBlock / L;  // filters per block
   constexpr int MPL = group_max_per_lane<M>();

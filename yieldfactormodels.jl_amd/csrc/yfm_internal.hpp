@@ -1,5 +1,6 @@
 // yfm_internal.hpp — launch interface between the C ABI (yfm_capi.hip) and the kernels.
 #pragma once
+#include "yfm_flags.hpp"
 #include <hip/hip_runtime.h>
 
 #include "../../include/yfm.h"
@@ -15,7 +16,7 @@ struct LaunchArgs {
   const double* mats;   // N device
   const int* T_use;     // B device or nullptr
   double* out;          // B device
-  unsigned int* flags;  // this launch's 4 counters [n_init_throw, n_neg_inf, defer list length, n_deferred]
+  unsigned int* flags;  // this launch's kFlagsPerBank counters (kFlagsPerBank above)
   unsigned int* flags_next = nullptr;  // the other counter bank: zeroed by this launch's first kernel
   double* rec_beta;     // optional trajectories
   double* rec_P;

@@ -75,7 +75,7 @@ constexpr int fz_rec_len() { return M + M * (M + 1) / 2 + 1; }
 template <int M, int LEAD>
 __global__ __launch_bounds__(256) void fixedz_init_kernel(const double* __restrict__ theta, int P, int B, int space,
                                                           double* __restrict__ rec, unsigned int* __restrict__ flags_next) {
-  if (flags_next && blockIdx.x == 0 && threadIdx.x < 4) flags_next[threadIdx.x] = 0u;  // the next launch's counters
+  if (flags_next && blockIdx.x == 0 && threadIdx.x < kFlagsPerBank) flags_next[threadIdx.x] = 0u;  // the next launch's counters
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   Params<M, LEAD> p;
@@ -132,14 +132,18 @@ typedef double yfm_double4 __attribute__((ext_vector_type(4)));
 // computed one step ahead, inside the same basic block as the update.
 // A wave-uniform fast path (no NaN column, every lane active, every lane collapsed,
 // t ≥ 1) carries no per-lane masking; everything else takes the general path.
-template <int NP, int M, int LEAD, bool RECORD>
+template <int NP, int M, int LEAD, bool RECORD, bool STEADY_ = false>
 __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     const double* __restrict__ theta, int P, int B, int space, const double* __restrict__ panel, int T, int N,
     const double* __restrict__ mats, const int* __restrict__ T_use, double* __restrict__ out,
     unsigned int* __restrict__ flags, double* __restrict__ rec_beta, double* __restrict__ rec_P, int horizon,
     int rec_len, int* __restrict__ defer_list, int* __restrict__ defer_count, const double* __restrict__ init_rec,
-    unsigned int* __restrict__ flags_next) {
+    unsigned int* __restrict__ flags_next, int steady) {
   constexpr int LDP = NP + 4;
+  constexpr bool USE_MFMA_ = (M - 1 == 2 || M - 1 == 4) && (NP <= 32);
+  // frozen-covariance steady state (FixedZFilter): the loglik-mode DNS instantiation
+  // with STEADY_ (the plain instantiation is the full recursion, YFM_DNS_STEADY=0)
+  constexpr bool STEADY = STEADY_ && !RECORD && M == 3 && USE_MFMA_;
   constexpr bool SPLIT_INIT = (M == 5);  // initial state from fixedz_init_kernel
   constexpr int CH = kTC * LDP;               // doubles per chunk
   constexpr int PER = (CH + kBlock - 1) / kBlock;
@@ -167,7 +171,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   __shared__ int s_nobs_max;
   __shared__ double s_rm[ZB ? NP : 1];  // 1/m_i (0 past N)
 
-  if (flags_next && blockIdx.x == 0 && threadIdx.x < 4) flags_next[threadIdx.x] = 0u;  // the next launch's counters
+  if (flags_next && blockIdx.x == 0 && threadIdx.x < kFlagsPerBank) flags_next[threadIdx.x] = 0u;  // the next launch's counters
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -270,8 +274,9 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     }
   }
 
-  FixedZFilter<M, LEAD, RECORD> f;
+  FixedZFilter<M, LEAD, RECORD, STEADY> f;
   f.p = p;
+  f.steady_ok = steady != 0;
   f.setup(G, N, !SPLIT_INIT);
   if constexpr (SPLIT_INIT) {
     int q = 0;
@@ -353,6 +358,8 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
 
   if constexpr (USE_MFMA) {
     double* scr = scratch[wave];
+    unsigned int steady_steps = 0;  // STEADY: this wave's steady steps (one atomic at the end: a per-block
+                                    // atomic would put its latency on the next global load's wait)
     for (int t0 = 0; t0 < nsteps; t0 += TB) {
       // ---- z̃ for steps t0 .. t0+15 of all 64 candidates: NRT·NK MFMAs ----
       const double* cb = col_of(t0);  // TB consecutive columns of one chunk
@@ -446,6 +453,16 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's scratch writes landed
       __builtin_amdgcn_wave_barrier();
       const int tend = min(TB, nsteps - t0);
+      // a block of steady steps: every lane of the wave frozen, and every step of the block a data
+      // step of every lane (no NaN column, t ≥ 1, inside every lane's window)
+      bool blk_steady = false;
+      if constexpr (STEADY) {
+        if (f.wave_frozen && t0 >= 1 && t0 + tend <= wave_min_data) {
+          bool nan_free = true;
+          for (int k = 0; k < tend; ++k) nan_free = nan_free && (cb[k * LDP + NP + 2] == 0.0);
+          blk_steady = nan_free;
+        }
+      }
       // step operands for tt are read one step ahead (hides the LDS latency at 1 wave/SIMD)
       auto read_z = [&](int tt, double (&z)[NZ]) {  // this lane's pairs NZ·lane .. NZ·lane + NZ − 1
         const double* sp = scr + tt * SS + NZ * lane;
@@ -479,14 +496,40 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
         record(t);
         rotate(t);
       };
-      int tt = 0;
-      for (; tt + 1 < tend; tt += 2) {
-        half(tt, zc, yb, meta, zn, ybn, metan);
-        half(tt + 1, zn, ybn, metan, zc, yb, meta);
+      if constexpr (STEADY) {
+        if (blk_steady) {
+          // the mean update only, with the cached factors of S (bitwise the full step's values for a
+          // frozen lane); operands read one step ahead as in `half`
+          auto shalf = [&](int tt, const double (&zc_)[NZ], double2 yb_, double (&zn_)[NZ], double2& ybn_) {
+            const int tn = min(tt + 1, TB - 1);
+            read_z(tn, zn_);
+            ybn_ = *reinterpret_cast<const double2*>(cb + tn * LDP + NP);
+            f.steady_step(zc_, yb_);
+            rotate(t0 + tt);
+          };
+          int tt = 0;
+          for (; tt + 1 < tend; tt += 2) {
+            shalf(tt, zc, yb, zn, ybn);
+            shalf(tt + 1, zn, ybn, zc, yb);
+          }
+          if (tt < tend) shalf(tt, zc, yb, zn, ybn);
+          steady_steps += tend;
+        }
       }
-      if (tt < tend) half(tt, zc, yb, meta, zn, ybn, metan);
+      if (!blk_steady) {
+        int tt = 0;
+        for (; tt + 1 < tend; tt += 2) {
+          half(tt, zc, yb, meta, zn, ybn, metan);
+          half(tt + 1, zn, ybn, metan, zc, yb, meta);
+        }
+        if (tt < tend) half(tt, zc, yb, meta, zn, ybn, metan);
+        if constexpr (STEADY) f.wave_freeze(live && !defer && f.init_ok && t0 + tend <= my_steps);
+      }
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();  // scratch reads done before the next block's writes
+    }
+    if constexpr (STEADY) {
+      if (lane == 0 && steady_steps) atomicAdd(&flags[4], steady_steps);  // yfm_last_batch_steady
     }
   } else {
     double zc[NZ];
@@ -534,6 +577,12 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
 
 namespace yfm {
 
+// the frozen-covariance steady state of the DNS loglik kernel (FixedZFilter): on unless YFM_DNS_STEADY=0
+static int steady_enabled() {
+  const char* e = std::getenv("YFM_DNS_STEADY");
+  return (e && e[0] == '0') ? 0 : 1;
+}
+
 template <int NP, int M, int LEAD>
 static hipError_t launch_fixedz_np(const LaunchArgs& a) {
   const int grid = (a.B + kBlock - 1) / kBlock;
@@ -545,11 +594,14 @@ static hipError_t launch_fixedz_np(const LaunchArgs& a) {
   if (a.rec_beta) {
     hipLaunchKernelGGL((fixedz_loglik_kernel<NP, M, LEAD, true>), dim3(grid), dim3(kBlock), 0, a.stream, a.theta, a.P,
                        a.B, a.space, a.panel, a.T, a.N, a.mats, a.T_use, a.out, a.flags, a.rec_beta, a.rec_P,
-                       a.horizon, a.rec_len, a.defer_list, a.defer_count, a.scratch, M == 5 ? nullptr : a.flags_next);
+                       a.horizon, a.rec_len, a.defer_list, a.defer_count, a.scratch, M == 5 ? nullptr : a.flags_next, 0);
   } else {
-    hipLaunchKernelGGL((fixedz_loglik_kernel<NP, M, LEAD, false>), dim3(grid), dim3(kBlock), 0, a.stream, a.theta,
-                       a.P, a.B, a.space, a.panel, a.T, a.N, a.mats, a.T_use, a.out, a.flags, nullptr, nullptr, 0, 0,
-                       a.defer_list, a.defer_count, a.scratch, M == 5 ? nullptr : a.flags_next);
+    constexpr bool kSteady = (M == 3) && (NP <= 32);  // the MFMA instantiations
+    auto* k = (kSteady && steady_enabled()) ? &fixedz_loglik_kernel<NP, M, LEAD, false, kSteady>
+                                            : &fixedz_loglik_kernel<NP, M, LEAD, false, false>;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, a.stream, a.theta, a.P, a.B, a.space, a.panel, a.T, a.N,
+                       a.mats, a.T_use, a.out, a.flags, nullptr, nullptr, 0, 0, a.defer_list, a.defer_count,
+                       a.scratch, M == 5 ? nullptr : a.flags_next, 1);
   }
   return hipGetLastError();
 }

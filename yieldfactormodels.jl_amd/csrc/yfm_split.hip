@@ -49,7 +49,7 @@ __global__ __launch_bounds__(kSplitBlock, 1) void dns_split_kernel(
     int rec_len, int* __restrict__ defer_list, int* __restrict__ defer_count, int interleave,
     unsigned int* __restrict__ flags_next) {
   constexpr int M = 3, LEAD = 1, NZ = 2;
-  if (flags_next && blockIdx.x == 0 && threadIdx.x < 4) flags_next[threadIdx.x] = 0u;  // the next launch's counters
+  if (flags_next && blockIdx.x == 0 && threadIdx.x < kFlagsPerBank) flags_next[threadIdx.x] = 0u;  // the next launch's counters
   constexpr int LDP = NP + 4;
   constexpr int CH = kSTC * LDP;
   constexpr int PER = (CH + kSplitBlock - 1) / kSplitBlock;

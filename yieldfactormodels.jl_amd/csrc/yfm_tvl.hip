@@ -53,7 +53,7 @@ enum : int { S2 = 0, S3, S4, G22, G23, G24, G33, G34, G44, U1, U2, U3, U4, VV, N
 // decode θ_b (transform_params + set_params!) and run initialize_filter (filter.jl:1-10)
 __global__ __launch_bounds__(256) void tvl_init_kernel(const double* __restrict__ theta, int P, int B, int space,
                                                        double* __restrict__ rec, unsigned int* __restrict__ flags_next) {
-  if (flags_next && blockIdx.x == 0 && threadIdx.x < 4) flags_next[threadIdx.x] = 0u;  // the next launch's counters
+  if (flags_next && blockIdx.x == 0 && threadIdx.x < kFlagsPerBank) flags_next[threadIdx.x] = 0u;  // the next launch's counters
   constexpr int M = 4;
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;

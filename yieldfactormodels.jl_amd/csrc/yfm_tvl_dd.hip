@@ -169,7 +169,7 @@ __device__ __forceinline__ void dd_propagate_q(const double* par, int qr, const 
 // decode θ_b in dd (transform_params + set_params!) and run initialize_filter (filter.jl:1-10)
 __global__ __launch_bounds__(64) void tvl_dd_init_kernel(const double* __restrict__ theta, int P, int B, int space,
                                                          double* __restrict__ rec, unsigned int* __restrict__ flags_next) {
-  if (flags_next && blockIdx.x == 0 && threadIdx.x < 4) flags_next[threadIdx.x] = 0u;  // the next launch's counters
+  if (flags_next && blockIdx.x == 0 && threadIdx.x < kFlagsPerBank) flags_next[threadIdx.x] = 0u;  // the next launch's counters
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const double* th = theta + (size_t)b * P;

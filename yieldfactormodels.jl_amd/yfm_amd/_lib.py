@@ -34,6 +34,7 @@ SIGNATURES = {
                                          _D]),
     "yfm_last_batch_flags": (ctypes.c_int, [_V, _LL, _LL]),
     "yfm_last_batch_deferred": (ctypes.c_int, [_V, _LL]),
+    "yfm_last_batch_steady": (ctypes.c_int, [_V, _LL]),
     "yfm_gamma_dim": (ctypes.c_int, [ctypes.c_int]),
     "yfm_predict": (ctypes.c_int, [_V, ctypes.c_int, ctypes.c_int, _D, ctypes.c_int, ctypes.c_int, _I, ctypes.c_int,
                                    _D, _D, _D, _D, _D]),

@@ -202,6 +202,13 @@ class Engine:
         _lib.check(self.lib.yfm_last_batch_deferred(self.ctx, ctypes.byref(n)))
         return n.value
 
+    def last_steady(self) -> int:
+        """Wave-steps (64 filter steps each) of the last batch that ran the DNS kernel's frozen-covariance
+        steady state (include/yfm.h yfm_last_batch_steady)."""
+        n = ctypes.c_longlong(0)
+        _lib.check(self.lib.yfm_last_batch_steady(self.ctx, ctypes.byref(n)))
+        return int(n.value)
+
 
 _engines: dict[int, Engine] = {}
 _lock = threading.Lock()
