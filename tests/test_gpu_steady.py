@@ -98,3 +98,16 @@ def test_steady_windows_nan_unit_root(engine, seed):
     got = engine.loglik(KIND_DNS, Th, T_use=tu)
     ref = full(lambda: engine.loglik(KIND_DNS, Th, T_use=tu))
     assert rel(got, ref).max() <= 1e-12
+
+
+def test_short_panel_runs_full_recursion(engine):
+    """T < 80: the launcher keeps the full-recursion instantiation (the first full block and the
+    freeze tests cost more than the steady steps save; profiles/r3/probes/dns_tsweep/)."""
+    mats = S.maturities_30()
+    Y = S.simulate_panel(KIND_DNS, 40, maturities=mats).copy(order="F")
+    engine.set_panel(Y, mats)
+    Th = S.theta_batch(KIND_DNS, 2048, seed=7)
+    got = engine.loglik(KIND_DNS, Th)
+    assert engine.last_steady() == 0
+    ref = full(lambda: engine.loglik(KIND_DNS, Th))
+    assert np.array_equal(got, ref, equal_nan=True)

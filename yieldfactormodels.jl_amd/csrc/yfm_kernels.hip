@@ -598,7 +598,10 @@ static hipError_t launch_fixedz_np(const LaunchArgs& a) {
                        a.horizon, a.rec_len, a.defer_list, a.defer_count, a.scratch, M == 5 ? nullptr : a.flags_next, 0);
   } else {
     constexpr bool kSteady = (M == 3) && (NP <= 32);  // the MFMA instantiations
-    auto* k = (kSteady && steady_enabled()) ? &fixedz_loglik_kernel<NP, M, LEAD, false, kSteady>
+    // short panels: the first (full) block and the freeze tests cost more than the steady steps save
+    // (T = 34: 0.054 vs 0.045 ms; equal at T = 66; profiles/r3/probes/dns_tsweep/)
+    constexpr int kSteadyMinT = 80;
+    auto* k = (kSteady && steady_enabled() && a.T >= kSteadyMinT) ? &fixedz_loglik_kernel<NP, M, LEAD, false, kSteady>
                                             : &fixedz_loglik_kernel<NP, M, LEAD, false, false>;
     hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, a.stream, a.theta, a.P, a.B, a.space, a.panel, a.T, a.N,
                        a.mats, a.T_use, a.out, a.flags, nullptr, nullptr, 0, 0, a.defer_list, a.defer_count,
