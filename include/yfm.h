@@ -203,7 +203,7 @@ int yfm_last_batch_deferred(yfm_ctx* ctx, long long* n_deferred);
  * DESIGN.md §3.1).  The covariance recursion of filter.jl:158-176 does not depend on the data when the
  * loadings are fixed; a candidate freezes its P once the change per step is at the rounding level, at a
  * step that depends on its own θ only.  YFM_DNS_STEADY=0 in the environment disables it.  0 for the
- * other models and for trajectories. */
+ * other models, for trajectories and for panels shorter than 80 columns (full recursion there). */
 int yfm_last_batch_steady(yfm_ctx* ctx, long long* steady_wave_steps);
 
 #ifdef __cplusplus
