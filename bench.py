@@ -77,6 +77,9 @@ def steady_update_flops(M: int) -> float:
     f = nz + 2 * M * nz + 2 * nz + 1 + M      # z̃/σ², ĉ, residual, ĉ₀ += ȳ, c = ĉ − β
     f += 2 * M * (M - 1) + M + 2 * M + 2      # x = S⁻¹c, c'x, q
     f += 2 * M * M + 2 * M * M                # β_{t|t} = β + P x, β ← δ + Φβ
+    if M > 3:                                 # GNS5 refactors the constant S each steady step (no cached factors)
+        f += M * (M + 1) // 2                 # S = P + R (lower)
+        f += sum(2 * j + 1 + (M - 1 - j) * (2 * j + 1) for j in range(M)) + (M - 1)  # LDLᵀ + det
     return f + 3
 
 
@@ -332,15 +335,16 @@ def pmc_traffic(kernel_substr: str, evals: int):
     return None, None
 
 
-DOMINANT = {KIND_DNS: "fixedz_loglik_kernel<30, 3, 1, false, true>", KIND_GNS: "fixedz_loglik_kernel<30, 5, 2, false, false>",
+DOMINANT = {KIND_DNS: "fixedz_loglik_kernel<30, 3, 1, false, true>", KIND_GNS: "fixedz_loglik_kernel<30, 5, 2, false, true>",
             (KIND_DNS, "full"): "fixedz_loglik_kernel<30, 3, 1, false, false>",
+            (KIND_GNS, "full"): "fixedz_loglik_kernel<30, 5, 2, false, false>",
             (KIND_TVL, "fp64"): "tvl_loglik_kernel", (KIND_TVL, "certified"): "tvl_dd_loglik_kernel"}
 
 
 def roofline(kind, prec, N, M, T, T_use, B, P, kernel_ms, steady_lane_steps=0):
     """The dominant kernel against the FP64 VALU roofline: achieved = algorithmic flops of the
     formulation it runs (alg_flops) for this GPU's batch ÷ HIP-event time per launch.  Filter steps
-    run in the DNS kernel's frozen-covariance steady state (`steady_lane_steps`, measured by the
+    run in the DNS/GNS5 kernel's frozen-covariance steady state (`steady_lane_steps`, measured by the
     kernel: yfm_last_batch_steady × 64) count the steady step's flops instead of the full update's."""
     Tb = T_use if T_use is not None else np.full(B, T)
     f_rank = float(np.sum(alg_flops(kind, N, M, Tb)))
@@ -349,7 +353,7 @@ def roofline(kind, prec, N, M, T, T_use, B, P, kernel_ms, steady_lane_steps=0):
     achieved = f_rank / (kernel_ms * 1e-3) / 1e12
     if kind == KIND_TVL:
         name = DOMINANT[(kind, prec)]
-    elif kind == KIND_DNS and os.environ.get("YFM_DNS_STEADY", "1").startswith("0"):
+    elif kind in (KIND_DNS, KIND_GNS) and os.environ.get("YFM_DNS_STEADY", "1").startswith("0"):
         name = DOMINANT[(kind, "full")]  # the full-recursion instantiation
     else:
         name = DOMINANT[kind]
@@ -523,13 +527,13 @@ def main():
     best_main = best[0]
     ms_per_step = 1e3 * wall / args.steps
     value = w.global_batch / (wall / args.steps)
-    steady_ws = eng.last_steady() if kind == KIND_DNS else 0  # frozen-covariance wave-steps of the last launch
+    steady_ws = eng.last_steady() if kind in (KIND_DNS, KIND_GNS) else 0  # frozen-covariance wave-steps of the last launch
     roof = roofline(kind, args.precision, N, M, T, w.T_use, B, P, kernel_ms, steady_lane_steps=64 * steady_ws)
     out_host = d_out.cpu().numpy()
-    # DNS: the same workload with the full covariance recursion every step (YFM_DNS_STEADY=0), beside the
+    # DNS, GNS5: the same workload with the full covariance recursion every step (YFM_DNS_STEADY=0), beside the
     # default — the steady state must not change a loglik by more than rounding (tests/test_gpu_steady.py)
     steady = None
-    if kind == KIND_DNS:
+    if kind in (KIND_DNS, KIND_GNS):
         Tb = w.T_use if w.T_use is not None else np.full(B, T)
         os.environ["YFM_DNS_STEADY"] = "0"
         try:

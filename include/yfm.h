@@ -198,9 +198,9 @@ int yfm_last_batch_flags(yfm_ctx* ctx, long long* n_init_throw, long long* n_neg
  * and accuracy split (0 for TVλ).  For yfm_loglik_batch_device, synchronise the stream first. */
 int yfm_last_batch_deferred(yfm_ctx* ctx, long long* n_deferred);
 
-/* Wave-steps of the last batch that ran in the DNS kernel's frozen-covariance steady state (64 filter
- * steps each: the mean update only, with the converged P and the factors of S = P + R cached —
- * DESIGN.md §3.1).  The covariance recursion of filter.jl:158-176 does not depend on the data when the
+/* Wave-steps of the last batch that ran in the DNS / GNS5 kernel's frozen-covariance steady state (64
+ * filter steps each: the mean update only at the converged P — DNS with the factors of S = P + R
+ * cached, GNS5 refactoring the constant S — DESIGN.md §3.1).  The covariance recursion of filter.jl:158-176 does not depend on the data when the
  * loadings are fixed; a candidate freezes its P once the change per step is at the rounding level, at a
  * step that depends on its own θ only.  YFM_DNS_STEADY=0 in the environment disables it.  0 for the
  * other models, for trajectories and for panels shorter than 80 columns (full recursion there). */

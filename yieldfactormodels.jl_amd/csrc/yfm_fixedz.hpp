@@ -220,6 +220,10 @@ struct FixedZFilter {
   // The freeze step depends on the lane's θ alone, so its loglik does not depend on the batch.  Once
   // EVERY lane of a wave is frozen the wave runs the mean update only, with the factors of S cached —
   // bitwise the full step's values for a frozen lane (the same S, factorised by the same code).
+  // M ≤ 3 caches the factors of S at the wave's freeze; M = 5 has no registers for them (the GNS5
+  // kernel uses the whole file) and refactors the constant S every steady step instead, so only the
+  // covariance half (P S⁻¹R, ΦPΦ' + Q) is skipped — bitwise the same values either way
+  static constexpr bool kCacheFactors = (M <= 3);
   bool steady_ok = false;    // the runtime switch (YFM_DNS_STEADY, default on)
   bool frozen = false;
   double prevd = __builtin_inf();
@@ -245,25 +249,39 @@ struct FixedZFilter {
   __device__ __forceinline__ void wave_freeze(bool part) {
     if (wave_frozen) return;
     if (__all(frozen || !part)) {
-      double S[M][M];
+      if constexpr (kCacheFactors) {
+        double S[M][M];
 #pragma unroll
-      for (int i = 0; i < M; ++i)
+        for (int i = 0; i < M; ++i)
 #pragma unroll
-        for (int j = 0; j <= i; ++j) S[i][j] = Pm[i][j] + R[i][j];
-      dets = fs.factor(S);
+          for (int j = 0; j <= i; ++j) S[i][j] = Pm[i][j] + R[i][j];
+        dets = fs.factor(S);
+      }
       wave_frozen = true;
     }
   }
   // one data step of a frozen wave: the mean update of collapsed_update with the cached factors
   __device__ __forceinline__ void steady_step(const double (&zc)[M - 1], double2 yb_c) {
-    double bf[M], q;
-    collapsed_mean<M>(zc, yb_c.x, yb_c.y, R, rsig2, beta, Pm, fs, bf, q);
+    double bf[M], q, det;
+    if constexpr (kCacheFactors) {
+      collapsed_mean<M>(zc, yb_c.x, yb_c.y, R, rsig2, beta, Pm, fs, bf, q);
+      det = dets;
+    } else {
+      double S[M][M];
+#pragma unroll
+      for (int i = 0; i < M; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j) S[i][j] = Pm[i][j] + R[i][j];
+      LDLT<M> fl;
+      det = fl.factor(S);
+      collapsed_mean<M>(zc, yb_c.x, yb_c.y, R, rsig2, beta, Pm, fl, bf, q);
+    }
     propagate_mean_f<M>([&](int i, int j) { return p.Phi[i][j]; }, p.delta, bf, beta);
-    last_det = dets;
+    last_det = det;
     last_q = q;
-    ld.mul(dets);
+    ld.mul(det);
     sumq += q;
-    neg = neg || (dets < 0.0);
+    neg = neg || (det < 0.0);
   }
 
   // G = Z'Z → R, log det G, collapsed or deferred; then initialize_filter.

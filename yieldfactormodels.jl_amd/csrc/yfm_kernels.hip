@@ -143,7 +143,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   constexpr bool USE_MFMA_ = (M - 1 == 2 || M - 1 == 4) && (NP <= 32);
   // frozen-covariance steady state (FixedZFilter): the loglik-mode DNS instantiation
   // with STEADY_ (the plain instantiation is the full recursion, YFM_DNS_STEADY=0)
-  constexpr bool STEADY = STEADY_ && !RECORD && M == 3 && USE_MFMA_;
+  constexpr bool STEADY = STEADY_ && !RECORD && (M == 3 || M == 5) && USE_MFMA_;
   constexpr bool SPLIT_INIT = (M == 5);  // initial state from fixedz_init_kernel
   constexpr int CH = kTC * LDP;               // doubles per chunk
   constexpr int PER = (CH + kBlock - 1) / kBlock;
@@ -597,7 +597,7 @@ static hipError_t launch_fixedz_np(const LaunchArgs& a) {
                        a.B, a.space, a.panel, a.T, a.N, a.mats, a.T_use, a.out, a.flags, a.rec_beta, a.rec_P,
                        a.horizon, a.rec_len, a.defer_list, a.defer_count, a.scratch, M == 5 ? nullptr : a.flags_next, 0);
   } else {
-    constexpr bool kSteady = (M == 3) && (NP <= 32);  // the MFMA instantiations
+    constexpr bool kSteady = (M == 3 || M == 5) && (NP <= 32);  // the MFMA instantiations
     // short panels: the first (full) block and the freeze tests cost more than the steady steps save
     // (T = 34: 0.054 vs 0.045 ms; equal at T = 66; profiles/r3/probes/dns_tsweep/)
     constexpr int kSteadyMinT = 80;
