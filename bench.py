@@ -3,6 +3,11 @@
     python bench.py [--gpus N --steps K --warmup W] [--config 2|3|4|5]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
+`--gpus N > 1` without a launcher (WORLD_SIZE unset) starts the N ranks itself
+(yfm_amd.distributed.spawn_local_ranks: one fresh process per GPU, 127.0.0.1 rendezvous), so
+`python bench.py --gpus 8` and the torchrun form run the same N-rank job; a rank whose process
+group does not have N members exits non-zero.
+
 Default (`--config 2`, the metric's headline workload): one "step" = one batched DNS
 loglik over B = 65,536 parameter vectors per GPU (T = 600 months × N = 30 maturities,
 FP64), inputs resident in HBM; for N > 1 the step also all-gathers the per-candidate
@@ -403,6 +408,13 @@ def main():
                          "(multi-rank rehearsal on a one-GPU box)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: start the N ranks here (this parent never touches the GPU) and exit with their status
+        sys.exit(D.spawn_local_ranks(str(Path(__file__).resolve()), sys.argv[1:], args.gpus,
+                                     env=dict(os.environ, YFM_LAUNCHER="bench.py --gpus (spawn_local_ranks)")))
+    if args.gpus < 1:
+        sys.exit("--gpus must be >= 1")
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -418,6 +430,15 @@ def main():
         torch.cuda.set_device(0)
         gpu = 0
     dev = torch.device("cuda", gpu)
+    collective_world = 1
+    if world > 1:
+        # the world size the collectives actually span (RCCL / gloo all-reduce of one per rank)
+        one = torch.ones(1, dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(one)
+        collective_world = int(one.item())
+    if collective_world != args.gpus or world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but the job has WORLD_SIZE {world} and the collective spans "
+                 f"{collective_world} rank(s)")
 
     w = make_workload(args.config, world, rank, args.T, args.batch)
     kind = w.kind
@@ -610,6 +631,8 @@ def main():
             "value": value,
             "unit": "evals/s",
             "n_gpus": world,
+            "collective_world_size": collective_world,
+            "launcher": os.environ.get("YFM_LAUNCHER", "torchrun" if world > 1 else "single"),
             "steps": args.steps,
             "warmup": args.warmup,
             "clock_settle": {"seconds": round(settle["seconds"], 3), "steps": settle["steps"],

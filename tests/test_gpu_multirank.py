@@ -50,6 +50,24 @@ def test_bench_two_ranks_argmax(engine):
     assert line["best_candidate"]["loglik"] == ll.max()
 
 
+def test_bench_self_launches_n_ranks():
+    """`python bench.py --gpus 2` with no launcher (the driver's command shape): bench.py starts the two
+    ranks itself (yfm_amd.distributed.spawn_local_ranks), both share cuda:0 over gloo, and the line
+    reports the two-rank job — n_gpus 2, the collective's world size 2, the global batch of both ranks."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "1"
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--config", "2", "--batch", "4096", "--T", "120",
+           "--steps", "3", "--warmup", "1", "--settle-seconds", "0", "--no-cpu-baseline", "--dist-backend", "gloo"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=str(ROOT))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    line = lines[0]
+    print({k: line[k] for k in ("n_gpus", "collective_world_size", "launcher", "value")})
+    assert line["n_gpus"] == 2 and line["collective_world_size"] == 2
+    assert line["config"]["global_batch"] == 2 * 4096 and "spawn_local_ranks" in line["launcher"]
+
+
 def _rolling_worker(rank, world, port, Y, mats, out_dir, ret):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch  # noqa: F401

@@ -74,6 +74,8 @@ struct DevBuf {
 struct yfm::Workspace {
   DevBuf flags;       // 2 banks × kFlagsPerBank unsigned int: n_init_throw, n_neg_inf, deferral list length, n_deferred, steady wave-steps
   int bank = 0;       // the bank of the last launch (the other one is zeroed by that launch's first kernel)
+  bool bank_dirty = false;        // the last launch failed: its zeroing of the other bank may not have been enqueued
+  hipStream_t last_stream = nullptr;  // the stream of the last launch (its first kernel zeroes our bank)
   DevBuf scratch;     // per-candidate work records (TVλ / GNS5 / two-wave DNS init)
   DevBuf scratch_dd;  // TVλ double-double records (YFM_PREC_CERTIFIED)
   DevBuf defer;       // candidates handed from the FP64 fixed-loading kernels to the dd kernel
@@ -92,6 +94,9 @@ struct yfm_ctx {
   DevBuf theta, out, tuse, rec_beta, rec_P;
   DevBuf flags;  // 2 banks × kFlagsPerBank unsigned int: n_init_throw, n_neg_inf, deferral list length, n_deferred, steady wave-steps
   int bank = 0;  // the bank of the last launch (the other one is zeroed by that launch's first kernel)
+  bool bank_dirty = false;            // as Workspace::bank_dirty
+  hipStream_t last_stream = nullptr;  // as Workspace::last_stream
+  hipEvent_t order_ev = nullptr;      // orders a launch on a new stream after the previous stream's work
   DevBuf scratch;  // per-candidate work records (TVλ init)
   DevBuf scratch_dd;  // TVλ double-double records (YFM_PREC_CERTIFIED)
   DevBuf traj, init_bad;       // trajectory-mode state records, per-candidate init-throw marks
@@ -195,22 +200,61 @@ struct PanelView {
   int T;
 };
 
+int launch_impl(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int B, const int* d_T_use,
+                double* d_out, double* d_rb, double* d_rP, hipStream_t s, int horizon, int rec_len,
+                const PanelView* pv, bool reset_flags, yfm::Workspace* ws);
+
+// Counters [n_init_throw, n_neg_inf, defer_count, n_deferred, steady] in two banks: a launch uses the bank
+// its predecessor zeroed (its first kernel zeroes the other one), so no memset is enqueued per call.
+// That hand-off only holds when the predecessor's kernels were all enqueued (bank_dirty otherwise) and on
+// the same stream (the zeroing kernel would be unordered with this launch): in either case this launch
+// zeroes its bank itself, on its own stream, after making that stream wait for the previous one's work.
+// The bank index flips only once the launch succeeded; after a failed one the next launch zeroes its
+// bank itself.  A pipelined chunk continues its batch's counters and only resets the deferral
+// list length.
 int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int B, const int* d_T_use,
            double* d_out, double* d_rb, double* d_rP, hipStream_t s, int horizon = 0, int rec_len = 0,
            const PanelView* pv = nullptr, bool reset_flags = true, yfm::Workspace* ws = nullptr) {
   DevBuf& w_flags = ws ? ws->flags : ctx->flags;
   int& w_bank = ws ? ws->bank : ctx->bank;
+  bool& dirty = ws ? ws->bank_dirty : ctx->bank_dirty;
+  hipStream_t& last = ws ? ws->last_stream : ctx->last_stream;
+  unsigned int* fb = static_cast<unsigned int*>(w_flags.p);
+  if (reset_flags && (dirty || s != last)) {
+    const int nb = w_bank ^ 1;  // the bank this launch will use
+    if (!dirty && last != nullptr) {
+      if (!ctx->order_ev) YFM_HIP_CHECK(hipEventCreateWithFlags(&ctx->order_ev, hipEventDisableTiming));
+      YFM_HIP_CHECK(hipEventRecord(ctx->order_ev, last));
+      YFM_HIP_CHECK(hipStreamWaitEvent(s, ctx->order_ev, 0));
+    }
+    YFM_HIP_CHECK(hipMemsetAsync(fb + yfm::kFlagsPerBank * nb, 0, yfm::kFlagsPerBank * sizeof(unsigned int), s));
+    dirty = false;
+  }
+  const int r = launch_impl(ctx, kind, space, d_theta, P, B, d_T_use, d_out, d_rb, d_rP, s, horizon, rec_len, pv,
+                            reset_flags, ws);
+  if (r != YFM_OK) {
+    dirty = true;
+    return r;
+  }
+  if (reset_flags) {
+    w_bank ^= 1;
+    last = s;
+  }
+  return YFM_OK;
+}
+
+int launch_impl(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int B, const int* d_T_use,
+                double* d_out, double* d_rb, double* d_rP, hipStream_t s, int horizon, int rec_len,
+                const PanelView* pv, bool reset_flags, yfm::Workspace* ws) {
+  DevBuf& w_flags = ws ? ws->flags : ctx->flags;
+  const int w_bank = (ws ? ws->bank : ctx->bank) ^ (reset_flags ? 1 : 0);  // the bank this launch uses
   DevBuf& w_scratch = ws ? ws->scratch : ctx->scratch;
   DevBuf& w_scratch_dd = ws ? ws->scratch_dd : ctx->scratch_dd;
   DevBuf& w_defer = ws ? ws->defer : ctx->defer;
   DevBuf& w_scratch_fd = ws ? ws->scratch_fd : ctx->scratch_fd;
-  // Counters [n_init_throw, n_neg_inf, defer_count, n_deferred] in two banks: a launch uses the bank
-  // its predecessor zeroed (its first kernel zeroes the other one), so no memset is enqueued per call.
-  // A pipelined chunk continues its batch's counters and only resets the deferral list length.
   unsigned int* fb = static_cast<unsigned int*>(w_flags.p);
   unsigned int* flags_next = nullptr;
   if (reset_flags) {
-    w_bank ^= 1;
     flags_next = fb + yfm::kFlagsPerBank * (w_bank ^ 1);
   } else {
     YFM_HIP_CHECK(hipMemsetAsync(fb + yfm::kFlagsPerBank * w_bank + 2, 0, sizeof(unsigned int), s));
@@ -407,6 +451,7 @@ void yfm_destroy(yfm_ctx* ctx) {
     b->release();
   ctx->scratch_dd.release();
   for (DevBuf& b : ctx->gap_buf) b.release();
+  if (ctx->order_ev) (void)hipEventDestroy(ctx->order_ev);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
   delete ctx;

@@ -197,6 +197,62 @@ __device__ __forceinline__ void propagate_cov_freeze(const Params<M, LEAD>& p, c
   }
 }
 
+// Upper bound of C = Σ_{k≥1} ‖A^k‖_F² for the closed-loop matrix A = Φ(I − KZ) = Φ R S⁻¹, S = P + R
+// (I − KZ = I − P S⁻¹ = R S⁻¹ in the collapsed form).  The Riccati differences δ_t = P_{t+1} − P_t obey
+// the exact identity δ_{t+1} = A_{t+1} δ_t A_t' (information form: f(P₁) − f(P₂) = Φ(I + P₁J)⁻¹(P₁ − P₂)
+// (I + JP₂)⁻¹Φ', J = Z'Z/σ²), so once the A_t agree with A to first order the drift still to come after
+// a step that moved P by δ is ‖Σ_{k≥1} δ_{t+k}‖_F ≤ C‖δ‖_F — whatever the eigenvalues of A (real or
+// complex, monotone or oscillating convergence).  From A … A⁴ by sub-multiplicativity:
+// C ≤ (‖A‖² + ‖A²‖² + ‖A³‖² + ‖A⁴‖²)/(1 − ‖A⁴‖²); +Inf when ‖A⁴‖_F ≥ 1 (no bound: never frozen).
+template <int M, int LEAD>
+__device__ __forceinline__ double contraction_bound(const Params<M, LEAD>& p, const double (&R)[M][M],
+                                                    const double (&Pm)[M][M]) {
+  double S[M][M];
+#pragma unroll
+  for (int i = 0; i < M; ++i)
+#pragma unroll
+    for (int j = 0; j <= i; ++j) S[i][j] = Pm[i][j] + R[i][j];
+  LDLT<M> f;
+  (void)f.factor(S);
+  // ‖A^k‖_F² = Σ_j ‖A^k e_j‖² with A v = Φ(R(S⁻¹v)) applied k times: no M×M temporaries beyond the
+  // factors (the GNS5 kernel has no registers for A and its powers)
+  // (rolled loops: one column and one power at a time keeps the temporaries to two M-vectors)
+  double n0 = 0.0, n1 = 0.0, n2 = 0.0, n3 = 0.0;
+#pragma unroll 1
+  for (int j = 0; j < M; ++j) {
+    double v[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) v[i] = (i == j) ? 1.0 : 0.0;
+#pragma unroll 1
+    for (int k = 0; k < 4; ++k) {
+      f.solve(v);
+      double w[M];
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        double s = 0.0;
+#pragma unroll
+        for (int l = 0; l < M; ++l) s = fma(R[i][l], v[l], s);
+        w[i] = s;
+      }
+      double nk = 0.0;
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        double s = 0.0;
+#pragma unroll
+        for (int l = 0; l < M; ++l) s = fma(p.Phi[i][l], w[l], s);
+        v[i] = s;
+        nk = fma(s, s, nk);
+      }
+      n0 += (k == 0) ? nk : 0.0;
+      n1 += (k == 1) ? nk : 0.0;
+      n2 += (k == 2) ? nk : 0.0;
+      n3 += (k == 3) ? nk : 0.0;
+    }
+  }
+  // rounding of the bound itself: the sums carry ≤ a few ulps; the 1.01 margin covers it
+  return (n3 < 1.0) ? 1.01 * (n0 + n1 + n2 + n3) / (1.0 - n3) : __builtin_inf();
+}
+
 template <int M, int LEAD, bool RECORD, bool STEADY = false>
 struct FixedZFilter {
   Params<M, LEAD> p;
@@ -213,40 +269,55 @@ struct FixedZFilter {
 
   // ---- frozen covariance (STEADY: loglik mode of the per-lane kernel) ----
   // With Z fixed the covariance recursion P ↦ Φ P(P + R)⁻¹R Φ' + Q does not depend on the data and
-  // converges geometrically to the Riccati fixed point.  A lane freezes its P after the data step at
-  // which the relative change of P is ≤ 2^-46 and the remaining geometric drift, estimated from the
-  // ratio ρ of successive changes, is ≤ 2^-50 (d·ρ/(1 − ρ)); a frozen lane keeps P (and so S = P + R
-  // and its factors) for every later data step, until a prediction-only step (a NaN column) moves P.
-  // The freeze step depends on the lane's θ alone, so its loglik does not depend on the batch.  Once
-  // EVERY lane of a wave is frozen the wave runs the mean update only, with the factors of S cached —
-  // bitwise the full step's values for a frozen lane (the same S, factorised by the same code).
+  // converges to the Riccati fixed point.  A lane freezes its P after a data step that moved it by a
+  // relative d (largest entry change / largest entry) when
+  //   d = 0 — a bitwise fixed point of the FP64 recursion, which the full recursion never leaves, or
+  //   d ≤ 2^-46 and M·d·C ≤ 2^-50 — C bounds Σ_{k≥1}‖A^k‖_F² for the lane's closed-loop matrix
+  //   A = Φ R S⁻¹ (contraction_bound, computed once, prepare_bound), so every later P of the
+  //   full recursion is within 2^-50 (relative, to first order in d) of the frozen one, for monotone and
+  //   oscillating (complex-eigenvalue) convergence alike;
+  // a frozen lane keeps P (and so S = P + R and its factors) for every later data step, until a
+  // prediction-only step (a NaN column) moves P.  The freeze step depends on the lane's θ alone, so its
+  // loglik does not depend on the batch.  Once EVERY lane of a wave is frozen the wave runs the mean
+  // update only, with the factors of S cached — bitwise the full step's values for a frozen lane (the
+  // same S, factorised by the same code).
   // M ≤ 3 caches the factors of S at the wave's freeze; M = 5 has no registers for them (the GNS5
   // kernel uses the whole file) and refactors the constant S every steady step instead, so only the
   // covariance half (P S⁻¹R, ΦPΦ' + Q) is skipped — bitwise the same values either way
   static constexpr bool kCacheFactors = (M <= 3);
   bool steady_ok = false;    // the runtime switch (YFM_DNS_STEADY, default on)
   bool frozen = false;
-  double prevd = __builtin_inf();
-  bool wave_frozen = false;  // wave-uniform
+  double cbound = -1.0;      // 2·C of contraction_bound (< 0: not computed yet)
+  double dlast = __builtin_inf();  // d of the lane's last data step before its freeze
+  bool wave_frozen = false;  // wave-uniform at every block boundary (wave_freeze)
   LDLT<M> fs;                // factors of S = P + R at the frozen P (valid while wave_frozen)
   double dets = 0.0;
 
-  // the freeze test after a data step that moved P by (dmax, nmax)
+  // the freeze test after a data step that moved P by (dmax, nmax); Pm holds the new P
   __device__ __forceinline__ void freeze_test(double dmax, double nmax) {
     const double d = dmax / nmax;
-    const double rho = d / prevd;
-    const bool ok = (d <= 0x1p-46) && (rho < 0.999) && (d * rho <= 0x1p-50 * (1.0 - rho));
-    prevd = frozen ? prevd : d;
+    dlast = frozen ? dlast : d;
+    const bool ok = (d == 0.0) || (d <= 0x1p-46 && cbound >= 0.0 && (double)M * d * cbound <= 0x1p-50);
     frozen = frozen || (ok && steady_ok);
   }
-  // a prediction-only step moves P: every lane thaws
+  // C of contraction_bound, once per lane, at a block boundary (outside the unrolled steps: its
+  // temporaries would otherwise coexist with two steps' operands), as soon as the lane's P has
+  // converged to 2^-26: A then agrees with the fixed point's closed loop to ≈ κ(S)·2^-26, and the
+  // factor 2 on C covers that
+  __device__ __forceinline__ void prepare_bound() {
+    if (cbound < 0.0 && steady_ok && dlast <= 0x1p-26) cbound = 2.0 * contraction_bound<M, LEAD>(p, R, Pm);
+  }
+  // a prediction-only step moves P: the lane thaws (and clears the wave's state at the block's vote)
   __device__ __forceinline__ void thaw() {
     frozen = false;
-    prevd = __builtin_inf();
     wave_frozen = false;
   }
-  // wave vote (every lane of the wave calls this at the same point): `part` = the lane's result counts
+  // wave vote at the end of every full block (every lane of the wave calls this at the same point):
+  // `part` = the lane's result counts.  A lane that thawed during the block (a NaN column inside its
+  // window) clears the state for the whole wave, so wave_frozen is wave-uniform again — lanes outside
+  // their windows (or past B, mirroring candidate B − 1) never thaw and must not keep it alone.
   __device__ __forceinline__ void wave_freeze(bool part) {
+    wave_frozen = __all(wave_frozen);
     if (wave_frozen) return;
     if (__all(frozen || !part)) {
       if constexpr (kCacheFactors) {

@@ -361,6 +361,9 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     unsigned int steady_steps = 0;  // STEADY: this wave's steady steps (one atomic at the end: a per-block
                                     // atomic would put its latency on the next global load's wait)
     for (int t0 = 0; t0 < nsteps; t0 += TB) {
+      // the freeze rule's contraction bound, once per lane, at a block boundary before the block's MFMA
+      // accumulators are live (FixedZFilter::prepare_bound)
+      if constexpr (STEADY) f.prepare_bound();
       // ---- z̃ for steps t0 .. t0+15 of all 64 candidates: NRT·NK MFMAs ----
       const double* cb = col_of(t0);  // TB consecutive columns of one chunk
       if constexpr (ZB) {
@@ -457,7 +460,9 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
       // step of every lane (no NaN column, t ≥ 1, inside every lane's window)
       bool blk_steady = false;
       if constexpr (STEADY) {
-        if (f.wave_frozen && t0 >= 1 && t0 + tend <= wave_min_data) {
+        // (wave_frozen is wave-uniform here — wave_freeze re-establishes it after every full block; the
+        // vote keeps the branch uniform even so)
+        if (__all(f.wave_frozen) && t0 >= 1 && t0 + tend <= wave_min_data) {
           // the block's NaN flags, one column per lane: one LDS round trip instead of tend serial ones
           // (0.236 → 0.217 ms at config 2, profiles/r3/probes/dns_steady_nan/)
           const bool col_nan = (lane < tend) && (cb[min(lane, TB - 1) * LDP + NP + 2] != 0.0);
@@ -522,6 +527,9 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
         for (; tt + 1 < tend; tt += 2) {
           half(tt, zc, yb, meta, zn, ybn, metan);
           half(tt + 1, zn, ybn, metan, zc, yb, meta);
+          if constexpr (STEADY) {
+            if (tt == TB / 2 - 2) f.prepare_bound();  // mid-block as well: lanes may freeze within this block
+          }
         }
         if (tt < tend) half(tt, zc, yb, meta, zn, ybn, metan);
         if constexpr (STEADY) f.wave_freeze(live && !defer && f.init_ok && t0 + tend <= my_steps);

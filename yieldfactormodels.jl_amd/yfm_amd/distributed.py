@@ -17,12 +17,67 @@ which balances the T_use-dependent cost that a split by window would not.
 """
 from __future__ import annotations
 
+import os
+import socket
+import subprocess
+import sys
 from dataclasses import dataclass
 from typing import Callable
 
 import numpy as np
 import torch
 import torch.distributed as dist
+
+
+def free_port(host: str = "127.0.0.1") -> int:
+    """An unused TCP port on `host` for a local rendezvous (MASTER_PORT)."""
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind((host, 0))
+        return s.getsockname()[1]
+
+
+def spawn_local_ranks(script: str, argv: list[str], nprocs: int, env: dict | None = None,
+                      timeout: float | None = None) -> int:
+    """Run `python script argv…` as `nprocs` ranks of one job on this node, the way
+    `torch.distributed.run --nnodes=1 --nproc-per-node nprocs --master-addr 127.0.0.1` would: each child
+    gets RANK = LOCAL_RANK = r, WORLD_SIZE = LOCAL_WORLD_SIZE = nprocs, MASTER_ADDR = 127.0.0.1 and a free
+    MASTER_PORT, and selects its GPU from LOCAL_RANK itself.  The children are fresh processes started
+    by a parent that must not have initialised the GPU (it only waits); stdout/stderr pass through.
+    Returns 0 when every rank exits 0, else the first non-zero exit status (ranks still running after
+    a failure are terminated, so a rank stuck in a collective cannot hang the job)."""
+    base = dict(os.environ if env is None else env)
+    base.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), WORLD_SIZE=str(nprocs),
+                LOCAL_WORLD_SIZE=str(nprocs))
+    procs = []
+    for r in range(nprocs):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, script, *argv], env=e))
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                try:
+                    code = p.wait(timeout=0.2)
+                except subprocess.TimeoutExpired:
+                    continue
+                pending.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in pending:
+                        q.terminate()
+            if timeout is not None:
+                timeout -= 0.2
+                if timeout <= 0:
+                    for q in pending:
+                        q.kill()
+                    return rc or 124
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
 
 
 def shard_range(n: int, world: int, rank: int) -> tuple[int, int]:
