@@ -52,8 +52,14 @@ def build(force: bool = False, verbose: bool = True) -> Path:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
 
-    with ThreadPoolExecutor(max_workers=min(len(srcs), 4)) as ex:
-        list(ex.map(cc, zip(srcs, objs)))
+    # an object is rebuilt when it is older than its source, a header or this script (a header change
+    # rebuilds everything: the headers are shared by most translation units)
+    hdr = max([p.stat().st_mtime for p in CSRC.glob("*.hpp")] + [p.stat().st_mtime for p in (ROOT / "include").glob("*.h")]
+              + [Path(__file__).stat().st_mtime])
+    todo = [(s, o) for s, o in zip(srcs, objs)
+            if force or not o.exists() or o.stat().st_mtime < max(s.stat().st_mtime, hdr)]
+    with ThreadPoolExecutor(max_workers=max(1, min(len(todo), 4))) as ex:
+        list(ex.map(cc, todo))
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(LIB)]
     if verbose:
         print(" ".join(cmd), flush=True)

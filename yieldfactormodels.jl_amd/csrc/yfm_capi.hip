@@ -75,7 +75,8 @@ struct yfm::Workspace {
   DevBuf flags;       // 2 banks × kFlagsPerBank unsigned int: n_init_throw, n_neg_inf, deferral list length, n_deferred, steady wave-steps
   int bank = 0;       // the bank of the last launch (the other one is zeroed by that launch's first kernel)
   bool bank_dirty = false;        // the last launch failed: its zeroing of the other bank may not have been enqueued
-  hipStream_t last_stream = nullptr;  // the stream of the last launch (its first kernel zeroes our bank)
+  hipStream_t last_stream = nullptr;  // the stream of the last launch (compared, never used: it may be gone)
+  hipEvent_t done_ev = nullptr;       // recorded after every launch on its stream (orders a stream change)
   DevBuf scratch;     // per-candidate work records (TVλ / GNS5 / two-wave DNS init)
   DevBuf scratch_dd;  // TVλ double-double records (YFM_PREC_CERTIFIED)
   DevBuf defer;       // candidates handed from the FP64 fixed-loading kernels to the dd kernel
@@ -96,7 +97,7 @@ struct yfm_ctx {
   int bank = 0;  // the bank of the last launch (the other one is zeroed by that launch's first kernel)
   bool bank_dirty = false;            // as Workspace::bank_dirty
   hipStream_t last_stream = nullptr;  // as Workspace::last_stream
-  hipEvent_t order_ev = nullptr;      // orders a launch on a new stream after the previous stream's work
+  hipEvent_t done_ev = nullptr;       // as Workspace::done_ev
   DevBuf scratch;  // per-candidate work records (TVλ init)
   DevBuf scratch_dd;  // TVλ double-double records (YFM_PREC_CERTIFIED)
   DevBuf traj, init_bad;       // trajectory-mode state records, per-candidate init-throw marks
@@ -208,10 +209,11 @@ int launch_impl(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P,
 // its predecessor zeroed (its first kernel zeroes the other one), so no memset is enqueued per call.
 // That hand-off only holds when the predecessor's kernels were all enqueued (bank_dirty otherwise) and on
 // the same stream (the zeroing kernel would be unordered with this launch): in either case this launch
-// zeroes its bank itself, on its own stream, after making that stream wait for the previous one's work.
-// The bank index flips only once the launch succeeded; after a failed one the next launch zeroes its
-// bank itself.  A pipelined chunk continues its batch's counters and only resets the deferral
-// list length.
+// zeroes its bank itself, on its own stream, after making that stream wait for the event recorded at the
+// end of the previous launch (an event, not the previous stream: the caller may have destroyed it — the
+// estimator's per-group streams are).  The bank index flips only once the launch succeeded; after a
+// failed one the next launch zeroes its bank itself.  A pipelined chunk continues its batch's counters
+// and only resets the deferral list length.
 int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int B, const int* d_T_use,
            double* d_out, double* d_rb, double* d_rP, hipStream_t s, int horizon = 0, int rec_len = 0,
            const PanelView* pv = nullptr, bool reset_flags = true, yfm::Workspace* ws = nullptr) {
@@ -219,15 +221,11 @@ int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int 
   int& w_bank = ws ? ws->bank : ctx->bank;
   bool& dirty = ws ? ws->bank_dirty : ctx->bank_dirty;
   hipStream_t& last = ws ? ws->last_stream : ctx->last_stream;
+  hipEvent_t& done = ws ? ws->done_ev : ctx->done_ev;
   unsigned int* fb = static_cast<unsigned int*>(w_flags.p);
   if (reset_flags && (dirty || s != last)) {
-    const int nb = w_bank ^ 1;  // the bank this launch will use
-    if (!dirty && last != nullptr) {
-      if (!ctx->order_ev) YFM_HIP_CHECK(hipEventCreateWithFlags(&ctx->order_ev, hipEventDisableTiming));
-      YFM_HIP_CHECK(hipEventRecord(ctx->order_ev, last));
-      YFM_HIP_CHECK(hipStreamWaitEvent(s, ctx->order_ev, 0));
-    }
-    YFM_HIP_CHECK(hipMemsetAsync(fb + yfm::kFlagsPerBank * nb, 0, yfm::kFlagsPerBank * sizeof(unsigned int), s));
+    if (done) YFM_HIP_CHECK(hipStreamWaitEvent(s, done, 0));
+    YFM_HIP_CHECK(hipMemsetAsync(fb + yfm::kFlagsPerBank * (w_bank ^ 1), 0, yfm::kFlagsPerBank * sizeof(unsigned int), s));
     dirty = false;
   }
   const int r = launch_impl(ctx, kind, space, d_theta, P, B, d_T_use, d_out, d_rb, d_rP, s, horizon, rec_len, pv,
@@ -240,6 +238,8 @@ int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int 
     w_bank ^= 1;
     last = s;
   }
+  if (!done) YFM_HIP_CHECK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+  YFM_HIP_CHECK(hipEventRecord(done, s));
   return YFM_OK;
 }
 
@@ -451,7 +451,7 @@ void yfm_destroy(yfm_ctx* ctx) {
     b->release();
   ctx->scratch_dd.release();
   for (DevBuf& b : ctx->gap_buf) b.release();
-  if (ctx->order_ev) (void)hipEventDestroy(ctx->order_ev);
+  if (ctx->done_ev) (void)hipEventDestroy(ctx->done_ev);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
   delete ctx;
@@ -774,6 +774,7 @@ Workspace* workspace_create() {
 void workspace_destroy(Workspace* w) {
   if (!w) return;
   for (DevBuf* b : {&w->flags, &w->scratch, &w->scratch_dd, &w->defer, &w->scratch_fd}) b->release();
+  if (w->done_ev) (void)hipEventDestroy(w->done_ev);
   delete w;
 }
 

@@ -197,13 +197,16 @@ __device__ __forceinline__ void propagate_cov_freeze(const Params<M, LEAD>& p, c
   }
 }
 
-// Upper bound of C = Σ_{k≥1} ‖A^k‖_F² for the closed-loop matrix A = Φ(I − KZ) = Φ R S⁻¹, S = P + R
-// (I − KZ = I − P S⁻¹ = R S⁻¹ in the collapsed form).  The Riccati differences δ_t = P_{t+1} − P_t obey
-// the exact identity δ_{t+1} = A_{t+1} δ_t A_t' (information form: f(P₁) − f(P₂) = Φ(I + P₁J)⁻¹(P₁ − P₂)
-// (I + JP₂)⁻¹Φ', J = Z'Z/σ²), so once the A_t agree with A to first order the drift still to come after
-// a step that moved P by δ is ‖Σ_{k≥1} δ_{t+k}‖_F ≤ C‖δ‖_F — whatever the eigenvalues of A (real or
+// Upper bound of C = Σ_{k≥1} ‖A^k‖_∞² for the closed-loop matrix A = Φ(I − KZ) = Φ R S⁻¹, S = P + R
+// (I − KZ = I − P S⁻¹ = R S⁻¹ in the collapsed form; ‖·‖_∞ = largest absolute row sum).  The Riccati
+// differences δ_t = P_{t+1} − P_t obey the exact identity δ_{t+1} = A_{t+1} δ_t A_t' (information form:
+// f(P₁) − f(P₂) = Φ(I + P₁J)⁻¹(P₁ − P₂)(I + JP₂)⁻¹Φ', J = Z'Z/σ²), and |(A δ A')_ij| ≤ ‖δ‖_max
+// Σ_k|A_ik| Σ_l|A_jl|, so once the A_t agree with A to first order the drift still to come after a step
+// that moved P by δ is ‖Σ_{k≥1} δ_{t+k}‖_max ≤ C ‖δ‖_max — whatever the eigenvalues of A (real or
 // complex, monotone or oscillating convergence).  From A … A⁴ by sub-multiplicativity:
-// C ≤ (‖A‖² + ‖A²‖² + ‖A³‖² + ‖A⁴‖²)/(1 − ‖A⁴‖²); +Inf when ‖A⁴‖_F ≥ 1 (no bound: never frozen).
+// C ≤ (‖A‖² + ‖A²‖² + ‖A³‖² + ‖A⁴‖²)/(1 − ‖A⁴‖²); +Inf when ‖A⁴‖_∞ ≥ 1 (no bound: never frozen early).
+// Row j of A^k is (A')^k e_j, A'v = S⁻¹(R(Φ'v)): no M×M temporaries beyond the factors of S (the
+// GNS5 kernel has no registers for A and its powers), rolled loops (two M-vectors live).
 template <int M, int LEAD>
 __device__ __forceinline__ double contraction_bound(const Params<M, LEAD>& p, const double (&R)[M][M],
                                                     const double (&Pm)[M][M]) {
@@ -214,10 +217,7 @@ __device__ __forceinline__ double contraction_bound(const Params<M, LEAD>& p, co
     for (int j = 0; j <= i; ++j) S[i][j] = Pm[i][j] + R[i][j];
   LDLT<M> f;
   (void)f.factor(S);
-  // ‖A^k‖_F² = Σ_j ‖A^k e_j‖² with A v = Φ(R(S⁻¹v)) applied k times: no M×M temporaries beyond the
-  // factors (the GNS5 kernel has no registers for A and its powers)
-  // (rolled loops: one column and one power at a time keeps the temporaries to two M-vectors)
-  double n0 = 0.0, n1 = 0.0, n2 = 0.0, n3 = 0.0;
+  double n0 = 0.0, n1 = 0.0, n2 = 0.0, n3 = 0.0;  // ‖A^k‖_∞, k = 1..4
 #pragma unroll 1
   for (int j = 0; j < M; ++j) {
     double v[M];
@@ -225,35 +225,37 @@ __device__ __forceinline__ double contraction_bound(const Params<M, LEAD>& p, co
     for (int i = 0; i < M; ++i) v[i] = (i == j) ? 1.0 : 0.0;
 #pragma unroll 1
     for (int k = 0; k < 4; ++k) {
-      f.solve(v);
       double w[M];
 #pragma unroll
       for (int i = 0; i < M; ++i) {
         double s = 0.0;
 #pragma unroll
-        for (int l = 0; l < M; ++l) s = fma(R[i][l], v[l], s);
+        for (int l = 0; l < M; ++l) s = fma(p.Phi[l][i], v[l], s);  // Φ'v
         w[i] = s;
       }
-      double nk = 0.0;
+      double sum = 0.0;
 #pragma unroll
       for (int i = 0; i < M; ++i) {
         double s = 0.0;
 #pragma unroll
-        for (int l = 0; l < M; ++l) s = fma(p.Phi[i][l], w[l], s);
+        for (int l = 0; l < M; ++l) s = fma(R[i][l], w[l], s);  // R Φ'v
         v[i] = s;
-        nk = fma(s, s, nk);
       }
-      n0 += (k == 0) ? nk : 0.0;
-      n1 += (k == 1) ? nk : 0.0;
-      n2 += (k == 2) ? nk : 0.0;
-      n3 += (k == 3) ? nk : 0.0;
+      f.solve(v);  // S⁻¹ R Φ'v
+#pragma unroll
+      for (int i = 0; i < M; ++i) sum += fabs(v[i]);
+      n0 = (k == 0) ? fmax(n0, sum) : n0;
+      n1 = (k == 1) ? fmax(n1, sum) : n1;
+      n2 = (k == 2) ? fmax(n2, sum) : n2;
+      n3 = (k == 3) ? fmax(n3, sum) : n3;
     }
   }
-  // rounding of the bound itself: the sums carry ≤ a few ulps; the 1.01 margin covers it
-  return (n3 < 1.0) ? 1.01 * (n0 + n1 + n2 + n3) / (1.0 - n3) : __builtin_inf();
+  const double q = n3 * n3;
+  // rounding of the bound itself: a few ulps; the 1.01 margin covers it
+  return (q < 1.0) ? 1.01 * (n0 * n0 + n1 * n1 + n2 * n2 + q) / (1.0 - q) : __builtin_inf();
 }
 
-template <int M, int LEAD, bool RECORD, bool STEADY = false>
+template <int M, int LEAD, bool RECORD, bool STEADY = false, bool SPLIT_FORM = false>
 struct FixedZFilter {
   Params<M, LEAD> p;
   double sigma2, rsig2;
@@ -272,7 +274,7 @@ struct FixedZFilter {
   // converges to the Riccati fixed point.  A lane freezes its P after a data step that moved it by a
   // relative d (largest entry change / largest entry) when
   //   d = 0 — a bitwise fixed point of the FP64 recursion, which the full recursion never leaves, or
-  //   d ≤ 2^-46 and M·d·C ≤ 2^-50 — C bounds Σ_{k≥1}‖A^k‖_F² for the lane's closed-loop matrix
+  //   d ≤ 2^-46 and d·C ≤ 2^-50 — C bounds Σ_{k≥1}‖A^k‖_∞² for the lane's closed-loop matrix
   //   A = Φ R S⁻¹ (contraction_bound, computed once, prepare_bound), so every later P of the
   //   full recursion is within 2^-50 (relative, to first order in d) of the frozen one, for monotone and
   //   oscillating (complex-eigenvalue) convergence alike;
@@ -297,7 +299,7 @@ struct FixedZFilter {
   __device__ __forceinline__ void freeze_test(double dmax, double nmax) {
     const double d = dmax / nmax;
     dlast = frozen ? dlast : d;
-    const bool ok = (d == 0.0) || (d <= 0x1p-46 && cbound >= 0.0 && (double)M * d * cbound <= 0x1p-50);
+    const bool ok = (d == 0.0) || (d <= 0x1p-46 && cbound >= 0.0 && d * cbound <= 0x1p-50);
     frozen = frozen || (ok && steady_ok);
   }
   // C of contraction_bound, once per lane, at a block boundary (outside the unrolled steps: its
@@ -396,13 +398,24 @@ struct FixedZFilter {
     if (do_init) init_ok = init_state<M, LEAD>(p, beta, Pm);
   }
 
+  __device__ __forceinline__ void update(const double (&zc)[M - 1], double2 yb_c, double (&bf)[M], double (&Pf)[M][M],
+                                         double& det, double& q) const {
+    if constexpr (SPLIT_FORM) {
+      LDLT<M> fl;
+      det = collapsed_cov<M>(R, Pm, fl, Pf);
+      collapsed_mean<M>(zc, yb_c.x, yb_c.y, R, rsig2, beta, Pm, fl, bf, q);
+    } else {
+      collapsed_update<M>(zc, yb_c.x, yb_c.y, R, rsig2, beta, Pm, bf, Pf, det, q);
+    }
+  }
+
   // One filter! call on column t given z̃_t (zc), (ȳ, ỹ'ỹ) = yb and (nan flag, y'y) = meta.
   // `fast`: the caller guarantees t ≥ 1, a data column and an active lane (no masking).
   __device__ __forceinline__ void step(int t, const double (&zc)[M - 1], double2 yb_c, double2 meta_c, bool fast,
                                        int my_steps, int my_data) {
     if (fast) {
       double bf[M], Pf[M][M], det, q;
-      collapsed_update<M>(zc, yb_c.x, yb_c.y, R, rsig2, beta, Pm, bf, Pf, det, q);
+      update(zc, yb_c, bf, Pf, det, q);
       // (a singular F at t ≥ 2 makes the loglik −Inf whatever the state; trajectories skip the update)
       if constexpr (STEADY) {
         propagate_mean_f<M>([&](int i, int j) { return p.Phi[i][j]; }, p.delta, bf, beta);
@@ -417,6 +430,11 @@ struct FixedZFilter {
       ld.mul(det);
       sumq += q;
       neg = neg || (det < 0.0);
+#ifdef YFM_DEBUG_LANE
+      if (blockIdx.x == 0 && threadIdx.x == YFM_DEBUG_LANE)
+        printf("dbg t %d fast det %.17g q %.17g P00 %.17g P44 %.17g b0 %.17g z0 %.17g\n", t, det, q, Pm[0][0],
+               Pm[M - 1][M - 1], beta[0], zc[0]);
+#endif
       return;
     }
     const bool act = t < my_steps;
@@ -440,12 +458,16 @@ struct FixedZFilter {
         sumq += last_q;
         neg = neg || (last_det < 0.0);
       }
+#ifdef YFM_DEBUG_LANE
+      if (blockIdx.x == 0 && threadIdx.x == YFM_DEBUG_LANE)
+        printf("dbg t %d pred P00 %.17g P44 %.17g b0 %.17g\n", t, Pm[0][0], Pm[M - 1][M - 1], beta[0]);
+#endif
       return;
     }
     double det, q;
     double bf[M];
     double Pf[M][M];
-    collapsed_update<M>(zc, yb_c.x, yb_c.y, R, rsig2, beta, Pm, bf, Pf, det, q);
+    update(zc, yb_c, bf, Pf, det, q);
     const bool upd = det != 0.0;  // inv(F) threw: return without the update (filter.jl:151-154)
     if constexpr (STEADY) {
       if (upd) {
@@ -464,6 +486,11 @@ struct FixedZFilter {
       sumq += last_q;
       neg = neg || (det < 0.0);
     }
+#ifdef YFM_DEBUG_LANE  // diagnostic builds only (tools/dbg_variants.sh)
+    if (blockIdx.x == 0 && threadIdx.x == YFM_DEBUG_LANE)
+      printf("dbg t %d data det %.17g q %.17g P00 %.17g P44 %.17g b0 %.17g z0 %.17g yb %.17g %.17g\n", t, det, q,
+             Pm[0][0], Pm[M - 1][M - 1], beta[0], zc[0], yb_c.x, yb_c.y);
+#endif
   }
 
   // the state after step t into slot t − max(0, my_steps − rec_len) (the last rec_len steps)

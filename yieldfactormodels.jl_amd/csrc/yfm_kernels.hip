@@ -36,6 +36,10 @@ constexpr int kBlock = 256;  // 4 waves: one per SIMD of a CU
 constexpr int kTC = 32;      // panel columns per LDS chunk
 constexpr bool kMfma4 = true;   // GNS5 Z'ỹ on v_mfma_f64_4x4x4_4b_f64 (DNS keeps v_mfma_f64_16x16x4_f64)
 constexpr bool kZBasis = true;  // GNS5 fragments e = 1 − e^{−λm} against (ỹ, ỹ/m): see the kernel
+#ifndef YFM_PIPE_VALU
+#define YFM_PIPE_VALU 8
+#endif
+constexpr int kPipeValu = YFM_PIPE_VALU;  // VALU instructions between two MFMAs of a pipelined steady step
 
 __global__ void prep_panel_kernel(const double* __restrict__ Y, int N, int T, int np, int ldp,
                                   double* __restrict__ out) {
@@ -132,7 +136,7 @@ typedef double yfm_double4 __attribute__((ext_vector_type(4)));
 // computed one step ahead, inside the same basic block as the update.
 // A wave-uniform fast path (no NaN column, every lane active, every lane collapsed,
 // t ≥ 1) carries no per-lane masking; everything else takes the general path.
-template <int NP, int M, int LEAD, bool RECORD, bool STEADY_ = false>
+template <int NP, int M, int LEAD, bool RECORD, bool STEADY_ = false, bool SPLIT_FORM = false, bool PIPE_ = false>
 __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     const double* __restrict__ theta, int P, int B, int space, const double* __restrict__ panel, int T, int N,
     const double* __restrict__ mats, const int* __restrict__ T_use, double* __restrict__ out,
@@ -163,11 +167,16 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   constexpr int NRTA = 64 * RPC / 16;         // fragment row tiles per wave
   constexpr int SS = 64 * NZ + 2;             // scratch row stride (doubles): one row per step
   constexpr int SCR = USE_MFMA ? (TB * SS) : 2;
+  // PIPE (DNS steady state): a steady block issues the NEXT block's Z'ỹ MFMAs between its own mean
+  // updates — the matrix pipe and the VALU then work side by side instead of one after the other — into
+  // a second scratch buffer per wave (2 × 16.6 KB per wave: 151.5 KB of LDS at NP = 32)
+  constexpr bool PIPE = PIPE_ && STEADY && NZ == 2 && !ZB;
+  constexpr int NBUF = PIPE ? 2 : 1;
   static_assert(NZ == 2 * LEAD, "loading columns come in (S, C) pairs per gamma");
   static_assert(NP % 2 == 0, "double2 panel reads");
   static_assert(kTC % TB == 0, "MFMA blocks tile the panel chunk");
   __shared__ __attribute__((aligned(16))) double sh[2][CH];
-  __shared__ __attribute__((aligned(16))) double scratch[kBlock / 64][SCR];
+  __shared__ __attribute__((aligned(16))) double scratch[kBlock / 64][NBUF][SCR];
   __shared__ int s_nobs_max;
   __shared__ double s_rm[ZB ? NP : 1];  // 1/m_i (0 past N)
 
@@ -244,7 +253,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     constexpr int ZS = 4 * NK + 1;  // maturity stride of the staging image (odd: conflict-free LDS)
     constexpr int QT = NRTA / 4;  // row tiles per quarter (16 candidates)
     static_assert(16 * RPC * ZS <= SCR, "staging fits the scratch");
-    double* st = scratch[wave];
+    double* st = scratch[wave][0];
 #pragma unroll
     for (int qu = 0; qu < 4; ++qu) {
       if ((lane >> 4) == qu) {
@@ -274,7 +283,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     }
   }
 
-  FixedZFilter<M, LEAD, RECORD, STEADY> f;
+  FixedZFilter<M, LEAD, RECORD, STEADY, SPLIT_FORM> f;
   f.p = p;
   f.steady_ok = steady != 0;
   f.setup(G, N, !SPLIT_INIT);
@@ -357,16 +366,20 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   };
 
   if constexpr (USE_MFMA) {
-    double* scr = scratch[wave];
     unsigned int steady_steps = 0;  // STEADY: this wave's steady steps (one atomic at the end: a per-block
                                     // atomic would put its latency on the next global load's wait)
+    int buf = 0;          // PIPE: this block's scratch buffer
+    bool have_z = false;  // PIPE: this block's z̃ were formed during the previous (steady) block
     for (int t0 = 0; t0 < nsteps; t0 += TB) {
       // the freeze rule's contraction bound, once per lane, at a block boundary before the block's MFMA
       // accumulators are live (FixedZFilter::prepare_bound)
       if constexpr (STEADY) f.prepare_bound();
+      double* scr = scratch[wave][PIPE ? buf : 0];
       // ---- z̃ for steps t0 .. t0+15 of all 64 candidates: NRT·NK MFMAs ----
       const double* cb = col_of(t0);  // TB consecutive columns of one chunk
-      if constexpr (ZB) {
+      if (have_z) {
+        // (PIPE) already in scratch[wave][buf]
+      } else if constexpr (ZB) {
         // rows: pair 16r + 4blk + i = (candidate, γ index); columns j of step pair sp: step
         // 2sp + (j >> 1), ỹ (j even) or ỹ/m (j odd)
 #pragma unroll
@@ -502,8 +515,73 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
         record(t);
         rotate(t);
       };
+      bool have_next = false;
+      if constexpr (PIPE) {
+        if (blk_steady && tend == TB && t0 + TB < nsteps) {
+          // the steady block unrolled, with the next block's Z'ỹ MFMAs spread over its steps: unit u of
+          // the 4·NK units (row-tile pair u / NK, k-step u % NK; two MFMAs each, one per tile of the pair)
+          // runs in step u·TB / (4·NK); a pair's accumulators go to the other scratch buffer after its last
+          // k-step (the D layout of the block form above)
+          constexpr int U = (NRT / 2) * NK;
+          double* scn = scratch[wave][buf ^ 1];
+          const double* nb = col_of(t0 + TB);  // resident: chunk (t0+16)/32 is in LDS while chunk t0/32 runs
+          double zq[2][NZ];
+          double2 ybq[2];
+#pragma unroll
+          for (int j = 0; j < NZ; ++j) zq[0][j] = zc[j];
+          ybq[0] = yb;
+          yfm_double4 pa0 = yfm_double4{0.0, 0.0, 0.0, 0.0}, pa1 = pa0;
+#pragma unroll
+          for (int tt = 0; tt < TB; ++tt) {
+            const int cur = tt & 1, nx = cur ^ 1;
+            const int tn = min(tt + 1, TB - 1);
+            read_z(tn, zq[nx]);
+            ybq[nx] = *reinterpret_cast<const double2*>(cb + tn * LDP + NP);
+#pragma unroll
+            for (int u = (tt * U) / TB; u < ((tt + 1) * U) / TB; ++u) {
+              const int rp = 2 * (u / NK), kk = u % NK;
+              if (kk == 0) {
+                pa0 = yfm_double4{0.0, 0.0, 0.0, 0.0};
+                pa1 = pa0;
+              }
+              const int m = 4 * kk + (lane >> 4);
+              const double bv = (m < NP) ? nb[(lane & 15) * LDP + m] : 0.0;
+              pa0 = __builtin_amdgcn_mfma_f64_16x16x4f64(Af[rp][kk], bv, pa0, 0, 0, 0);
+              pa1 = __builtin_amdgcn_mfma_f64_16x16x4f64(Af[rp + 1][kk], bv, pa1, 0, 0, 0);
+              if (kk == NK - 1) {
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4) {
+                  scn[(lane & 15) * SS + 16 * rp + (lane >> 4) + 4 * q4] = pa0[q4];
+                  scn[(lane & 15) * SS + 16 * (rp + 1) + (lane >> 4) + 4 * q4] = pa1[q4];
+                }
+              }
+            }
+            f.steady_step(zq[cur], ybq[cur]);
+            // pin the step's results here: without a use the compiler sinks the whole mean-update chain
+            // past the block's end (it is only read by later blocks), away from the MFMAs it should hide
+#pragma unroll
+            for (int i = 0; i < M; ++i) asm volatile("" ::"v"(f.beta[i]));
+            asm volatile("" ::"v"(f.sumq), "v"(f.ld.mant));
+            // one scheduling region per step, the step's MFMAs spread through its mean update (the
+            // in-order wave would otherwise stall on the busy matrix pipe issuing them back to back)
+            const int MF = 2 * (((tt + 1) * U) / TB - (tt * U) / TB);
+#pragma unroll
+            for (int g = 0; g < MF; ++g) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);          // 1 MFMA
+              __builtin_amdgcn_sched_group_barrier(0x002, kPipeValu, 0);  // then VALU
+            }
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          // the chunk rotation of the block's last step (t0 is a multiple of TB, so only t0 + TB − 1 can
+          // end a chunk; nothing in the block reads LDS past it): outside the unrolled steps, which stay one
+          // basic block — a branch inside would let the compiler sink the arithmetic below the MFMAs
+          rotate(t0 + TB - 1);
+          steady_steps += TB;
+          have_next = true;
+        }
+      }
       if constexpr (STEADY) {
-        if (blk_steady) {
+        if (blk_steady && !have_next) {
           // the mean update only, with the cached factors of S (bitwise the full step's values for a
           // frozen lane); operands read one step ahead as in `half`
           auto shalf = [&](int tt, const double (&zc_)[NZ], double2 yb_, double (&zn_)[NZ], double2& ybn_) {
@@ -536,6 +614,10 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
       }
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();  // scratch reads done before the next block's writes
+      if constexpr (PIPE) {
+        buf ^= 1;
+        have_z = have_next;
+      }
     }
     if constexpr (STEADY) {
       if (lane == 0 && steady_steps) atomicAdd(&flags[4], steady_steps);  // yfm_last_batch_steady
@@ -592,6 +674,24 @@ static int steady_enabled() {
   return (e && e[0] == '0') ? 0 : 1;
 }
 
+// the GNS5 steady state: off unless YFM_GNS5_STEADY=1
+static int gns5_steady_enabled() {
+  const char* e = std::getenv("YFM_GNS5_STEADY");
+  return (e && e[0] == '1') ? 1 : 0;
+}
+
+// the pipelined steady blocks of the DNS kernel (PIPE): on unless YFM_DNS_PIPE=0
+static int pipe_enabled() {
+  const char* e = std::getenv("YFM_DNS_PIPE");
+  return (e && e[0] == '0') ? 0 : 1;
+}
+
+// diagnostic: YFM_FZ_SPLIT_FORM=1 selects the two-function update form (FixedZFilter SPLIT_FORM)
+static int split_form_enabled() {
+  const char* e = std::getenv("YFM_FZ_SPLIT_FORM");
+  return (e && e[0] == '1') ? 1 : 0;
+}
+
 template <int NP, int M, int LEAD>
 static hipError_t launch_fixedz_np(const LaunchArgs& a) {
   const int grid = (a.B + kBlock - 1) / kBlock;
@@ -609,8 +709,22 @@ static hipError_t launch_fixedz_np(const LaunchArgs& a) {
     // short panels: the first (full) block and the freeze tests cost more than the steady steps save
     // (T = 34: 0.054 vs 0.045 ms; equal at T = 66; profiles/r3/probes/dns_tsweep/)
     constexpr int kSteadyMinT = 80;
-    auto* k = (kSteady && steady_enabled() && a.T >= kSteadyMinT) ? &fixedz_loglik_kernel<NP, M, LEAD, false, kSteady>
-                                            : &fixedz_loglik_kernel<NP, M, LEAD, false, false>;
+    // GNS5: opt-in (YFM_GNS5_STEADY=1) — the freeze rule's contraction bound is loose for its slower closed
+    // loop (spectral radius ≈ 0.74 at θ₀): almost no config-5 wave freezes, and the steady instantiation's
+    // freeze tests and bound then cost 19.7 → 26.6 ms (profiles/r4/)
+    const bool on = steady_enabled() && a.T >= kSteadyMinT && (M != 5 || gns5_steady_enabled());
+    auto* k = (kSteady && on) ? &fixedz_loglik_kernel<NP, M, LEAD, false, kSteady>
+                              : &fixedz_loglik_kernel<NP, M, LEAD, false, false>;
+    // DNS: the steady blocks overlap the next block's Z'ỹ MFMAs with their mean updates (YFM_DNS_PIPE=0: off)
+    if constexpr (kSteady && M == 3) {
+      if (k == &fixedz_loglik_kernel<NP, M, LEAD, false, kSteady> && pipe_enabled())
+        k = &fixedz_loglik_kernel<NP, M, LEAD, false, kSteady, false, true>;
+    }
+    // diagnostic: the two-function form of the update (commit 7a42719's regression test), GNS5 full recursion
+    constexpr bool kSplitForm = (M == 5) && (NP == 30 || NP == 48);
+    if constexpr (kSplitForm) {
+      if (split_form_enabled()) k = &fixedz_loglik_kernel<NP, M, LEAD, false, false, true>;
+    }
     hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, a.stream, a.theta, a.P, a.B, a.space, a.panel, a.T, a.N,
                        a.mats, a.T_use, a.out, a.flags, nullptr, nullptr, 0, 0, a.defer_list, a.defer_count,
                        a.scratch, M == 5 ? nullptr : a.flags_next, 1);

@@ -239,17 +239,18 @@ class EstimationError(RuntimeError):
 
 
 def estimate_steps_(model: AbstractKalmanModel, data, all_params, param_groups=None, max_group_iters: int = 10,
-                    tol: float = 1e-8, printing: bool = False):
+                    tol: float = 1e-8, printing: bool = False, iterations: int = 500):
     """estimate_steps! (optimization.jl:137-312) for a Kalman model: all_params (P×n, constrained; Kalman
     models use column 1 only, :153) → (init_p, ll, best_p, ir), init_p and best_p constrained like the
     reference: init_p = transform_params of the untransformed, sanitised and ×0.95-rescaled start
     (:157-184, :298-302).
-    Parameter groups other than all-"1" are not supported (the Kalman default, kalmanbasemodel.jl:150-159)."""
+    Parameter groups other than all-"1" are not supported (the Kalman default, kalmanbasemodel.jl:150-159).
+    `iterations`: the NelderMead budget per group (opt1, optimization.jl:442-451: 500)."""
     A = np.asarray(all_params, dtype=np.float64)
     start = A[:, 0] if A.ndim == 2 else A
     if param_groups is not None and any(g != "1" for g in param_groups):
         raise NotImplementedError("Kalman models estimate every parameter in group \"1\"")
-    r = estimate_batch(model, data, start[:, None], max_group_iters=max_group_iters, tol=tol)
+    r = estimate_batch(model, data, start[:, None], max_group_iters=max_group_iters, tol=tol, iterations=iterations)
     if r["status"][0] == 1:
         raise EstimationError("compute_loss threw on the first group iteration (singular initialize_filter)")
     if printing:
