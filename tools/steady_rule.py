@@ -63,14 +63,15 @@ def loadings(g, mats):
 
 
 def contraction_C(Phi, R, Sm, M):
-    """Upper bound of Σ_{k≥1} ‖A^k‖_F² for A = Φ R S⁻¹ (inf where ‖A⁴‖_F ≥ 1)."""
+    """Upper bound of Σ_{k≥1} ‖A^k‖_∞² for A = Φ R S⁻¹ (inf where ‖A⁴‖_∞ ≥ 1), as the device's
+    contraction_bound (yfm_fixedz.hpp) with its 1.01 rounding margin."""
     A = Phi @ np.swapaxes(np.linalg.solve(Sm, R), 1, 2)  # R S⁻¹ = (S⁻¹R)'
     A2 = A @ A
     A3 = A2 @ A
     A4 = A2 @ A2
-    n = [np.sum(X * X, axis=(1, 2)) for X in (A, A2, A3, A4)]
+    n = [np.max(np.sum(np.abs(X), axis=2), axis=1) ** 2 for X in (A, A2, A3, A4)]
     with np.errstate(divide="ignore", invalid="ignore"):
-        C = np.where(n[3] < 1.0, (n[0] + n[1] + n[2] + n[3]) / (1.0 - n[3]), np.inf)
+        C = np.where(n[3] < 1.0, 1.01 * (n[0] + n[1] + n[2] + n[3]) / (1.0 - n[3]), np.inf)
     return C
 
 
@@ -131,9 +132,9 @@ def run(kind, Y, mats, Thc, rule=None, tau=2.0 ** -50):
                 ok = (d <= 2.0 ** -46) & (rho < 0.999) & (d * rho <= tau * (1 - rho))
             db = np.where(ok, d * rho / np.maximum(1 - rho, 1e-300), 0)
         else:
-            C = contraction_C(Phi, R, P + R, M)
-            ok = (d == 0) | ((d <= 2.0 ** -46) & (M * d * C <= tau))
-            db = np.where(d == 0, 0.0, M * d * C)
+            C = 2.0 * contraction_C(Phi, R, P + R, M)  # the device's 2C (first-order margin)
+            ok = (d == 0) | ((d <= 2.0 ** -46) & (d * C <= tau))
+            db = np.where(d == 0, 0.0, d * C)
         newf = ok & ~frozen
         drift_bound = np.where(newf, db, drift_bound)
         fstep[newf] = t + 1
@@ -153,6 +154,8 @@ def regimes(kind, B, rng):
     base = S.theta_batch(kind, B, seed=S.BATCH_SEED, bad_frac=0.0)
     out["config (θ₀ ± 0.1)"] = PR.transform_params(kind, base)
     out["wide (θ₀ ± 0.3)"] = PR.transform_params(kind, S.theta_batch(kind, B, seed=11, bad_frac=0.0, scale=0.3))
+    out["scale 1.0 (explosive Φ among them)"] = PR.transform_params(kind, S.theta_batch(kind, B, seed=15, bad_frac=0.02,
+                                                                                         scale=1.0))
     th = PR.transform_params(kind, S.theta_batch(kind, B, seed=12, bad_frac=0.0))
     th[lay.base_offset] = 10.0 ** rng.uniform(-6, -3, B)
     out["small σ² (1e-6..1e-3)"] = th
@@ -184,6 +187,7 @@ def main():
     ap.add_argument("--T", type=int, default=600)
     ap.add_argument("--kind", type=int, default=KIND_DNS)
     ap.add_argument("--rules", default="r3,contract")
+    ap.add_argument("--taus", default="50", help="comma list of k: freeze when d·2C ≤ 2^-k (contract rule)")
     a = ap.parse_args()
     kind = a.kind
     mats = S.maturities_30()
@@ -193,8 +197,9 @@ def main():
         full, *_ = run(kind, Y, mats, Thc)
         fin = np.isfinite(full)
         print(f"== {name}: {fin.sum()} finite of {a.B}")
-        for rule in a.rules.split(","):
-            ll, fs, db, sens = run(kind, Y, mats, Thc, rule)
+        for rule, k in [(r, k) for r in a.rules.split(",") for k in (a.taus.split(",") if r == "contract" else ["50"])]:
+            ll, fs, db, sens = run(kind, Y, mats, Thc, rule, 2.0 ** -int(k))
+            rule = f"{rule}{k}" if rule == "contract" else rule
             e = np.abs(ll[fin] - full[fin])
             rel = e / np.abs(full[fin])
             w = fs[: (a.B // 64) * 64].reshape(-1, 64).max(1)

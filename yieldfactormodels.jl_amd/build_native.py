@@ -19,8 +19,14 @@ BUILD = PKG / "build"
 LIB = PKG / "yfm_amd" / "libyfm_hip.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("YFM_OFFLOAD_ARCH", "gfx950")
+# -amdgpu-spill-vgpr-to-agpr=0: register spills go to scratch memory, never to AGPRs.  ROCm 7.2's backend
+# miscompiles the VGPR->AGPR spill path of the heavily spilling fixed-loading instantiations (GNS5 NP = 48,
+# ~850 spilled VGPRs): the same filter written as two functions returned O(1)-wrong logliks there, while
+# the host build of the same C++ is MemorySanitizer-clean and bitwise equal in both forms
+# (tools/host_fixedz/; tests/test_gpu_split_form.py).  Only the 12 spilling kernels change;
+# the config 2-5 kernels are byte-identical either way.
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
-         f"-I{ROOT / 'include'}"]
+         "-mllvm", "-amdgpu-spill-vgpr-to-agpr=0", f"-I{ROOT / 'include'}"]
 
 
 def _sources():

@@ -274,10 +274,11 @@ struct FixedZFilter {
   // converges to the Riccati fixed point.  A lane freezes its P after a data step that moved it by a
   // relative d (largest entry change / largest entry) when
   //   d = 0 — a bitwise fixed point of the FP64 recursion, which the full recursion never leaves, or
-  //   d ≤ 2^-46 and d·C ≤ 2^-50 — C bounds Σ_{k≥1}‖A^k‖_∞² for the lane's closed-loop matrix
+  //   d ≤ 2^-46 and d·C ≤ 2^-52 — C bounds Σ_{k≥1}‖A^k‖_∞² for the lane's closed-loop matrix
   //   A = Φ R S⁻¹ (contraction_bound, computed once, prepare_bound), so every later P of the
-  //   full recursion is within 2^-50 (relative, to first order in d) of the frozen one, for monotone and
-  //   oscillating (complex-eigenvalue) convergence alike;
+  //   full recursion is within 2^-52 (relative to its largest entry, to first order in d) of the frozen
+  //   one — inside the FP64 recursion's own rounding jitter — for monotone and oscillating
+  //   (complex-eigenvalue) convergence alike (DESIGN.md §3.1 carries the bound on the loglik);
   // a frozen lane keeps P (and so S = P + R and its factors) for every later data step, until a
   // prediction-only step (a NaN column) moves P.  The freeze step depends on the lane's θ alone, so its
   // loglik does not depend on the batch.  Once EVERY lane of a wave is frozen the wave runs the mean
@@ -299,7 +300,7 @@ struct FixedZFilter {
   __device__ __forceinline__ void freeze_test(double dmax, double nmax) {
     const double d = dmax / nmax;
     dlast = frozen ? dlast : d;
-    const bool ok = (d == 0.0) || (d <= 0x1p-46 && cbound >= 0.0 && d * cbound <= 0x1p-50);
+    const bool ok = (d == 0.0) || (d <= 0x1p-46 && cbound >= 0.0 && d * cbound <= 0x1p-52);
     frozen = frozen || (ok && steady_ok);
   }
   // C of contraction_bound, once per lane, at a block boundary (outside the unrolled steps: its
@@ -431,8 +432,8 @@ struct FixedZFilter {
       sumq += q;
       neg = neg || (det < 0.0);
 #ifdef YFM_DEBUG_LANE
-      if (blockIdx.x == 0 && threadIdx.x == YFM_DEBUG_LANE)
-        printf("dbg t %d fast det %.17g q %.17g P00 %.17g P44 %.17g b0 %.17g z0 %.17g\n", t, det, q, Pm[0][0],
+      if (blockIdx.x == 0 && threadIdx.x < YFM_DEBUG_LANE)
+        printf("dbg L%d t %d fast det %.17g q %.17g P00 %.17g P44 %.17g b0 %.17g z0 %.17g\n", (int)threadIdx.x, t, det, q, Pm[0][0],
                Pm[M - 1][M - 1], beta[0], zc[0]);
 #endif
       return;
@@ -459,8 +460,8 @@ struct FixedZFilter {
         neg = neg || (last_det < 0.0);
       }
 #ifdef YFM_DEBUG_LANE
-      if (blockIdx.x == 0 && threadIdx.x == YFM_DEBUG_LANE)
-        printf("dbg t %d pred P00 %.17g P44 %.17g b0 %.17g\n", t, Pm[0][0], Pm[M - 1][M - 1], beta[0]);
+      if (blockIdx.x == 0 && threadIdx.x < YFM_DEBUG_LANE)
+        printf("dbg L%d t %d pred P00 %.17g P44 %.17g b0 %.17g\n", (int)threadIdx.x, t, Pm[0][0], Pm[M - 1][M - 1], beta[0]);
 #endif
       return;
     }
@@ -487,8 +488,8 @@ struct FixedZFilter {
       neg = neg || (det < 0.0);
     }
 #ifdef YFM_DEBUG_LANE  // diagnostic builds only (tools/dbg_variants.sh)
-    if (blockIdx.x == 0 && threadIdx.x == YFM_DEBUG_LANE)
-      printf("dbg t %d data det %.17g q %.17g P00 %.17g P44 %.17g b0 %.17g z0 %.17g yb %.17g %.17g\n", t, det, q,
+    if (blockIdx.x == 0 && threadIdx.x < YFM_DEBUG_LANE)
+      printf("dbg L%d t %d data det %.17g q %.17g P00 %.17g P44 %.17g b0 %.17g z0 %.17g yb %.17g %.17g\n", (int)threadIdx.x, t, det, q,
              Pm[0][0], Pm[M - 1][M - 1], beta[0], zc[0], yb_c.x, yb_c.y);
 #endif
   }
