@@ -121,7 +121,11 @@ int yfm_loglik_batch(yfm_ctx* ctx, int model_kind, int param_space, const double
 
 /* Same with DEVICE pointers on the caller's HIP stream (hipStream_t passed as
  * void*, NULL = default stream); asynchronous: returns after enqueueing.  For
- * pipelines that keep Θ resident in HBM (bench.py, RCCL sharding). */
+ * pipelines that keep Θ resident in HBM (bench.py, RCCL sharding).  A context's
+ * device scratch and counters serve one launch at a time: consecutive launches on
+ * the same stream are ordered by the stream; a caller that moves to another stream
+ * orders the two itself (hipStreamWaitEvent or a synchronisation), as for any HIP
+ * work sharing buffers.  The library never touches a previous launch's stream. */
 int yfm_loglik_batch_device(yfm_ctx* ctx, int model_kind, int param_space, const double* d_theta, int P, int B,
                             const int* d_T_use, double* d_loglik_out, void* hip_stream);
 

@@ -76,7 +76,6 @@ struct yfm::Workspace {
   int bank = 0;       // the bank of the last launch (the other one is zeroed by that launch's first kernel)
   bool bank_dirty = false;        // the last launch failed: its zeroing of the other bank may not have been enqueued
   hipStream_t last_stream = nullptr;  // the stream of the last launch (compared, never used: it may be gone)
-  hipEvent_t done_ev = nullptr;       // recorded after every launch on its stream (orders a stream change)
   DevBuf scratch;     // per-candidate work records (TVλ / GNS5 / two-wave DNS init)
   DevBuf scratch_dd;  // TVλ double-double records (YFM_PREC_CERTIFIED)
   DevBuf defer;       // candidates handed from the FP64 fixed-loading kernels to the dd kernel
@@ -97,7 +96,6 @@ struct yfm_ctx {
   int bank = 0;  // the bank of the last launch (the other one is zeroed by that launch's first kernel)
   bool bank_dirty = false;            // as Workspace::bank_dirty
   hipStream_t last_stream = nullptr;  // as Workspace::last_stream
-  hipEvent_t done_ev = nullptr;       // as Workspace::done_ev
   DevBuf scratch;  // per-candidate work records (TVλ init)
   DevBuf scratch_dd;  // TVλ double-double records (YFM_PREC_CERTIFIED)
   DevBuf traj, init_bad;       // trajectory-mode state records, per-candidate init-throw marks
@@ -207,13 +205,14 @@ int launch_impl(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P,
 
 // Counters [n_init_throw, n_neg_inf, defer_count, n_deferred, steady] in two banks: a launch uses the bank
 // its predecessor zeroed (its first kernel zeroes the other one), so no memset is enqueued per call.
-// That hand-off only holds when the predecessor's kernels were all enqueued (bank_dirty otherwise) and on
-// the same stream (the zeroing kernel would be unordered with this launch): in either case this launch
-// zeroes its bank itself, on its own stream, after making that stream wait for the event recorded at the
-// end of the previous launch (an event, not the previous stream: the caller may have destroyed it — the
-// estimator's per-group streams are).  The bank index flips only once the launch succeeded; after a
-// failed one the next launch zeroes its bank itself.  A pipelined chunk continues its batch's counters
-// and only resets the deferral list length.
+// That hand-off only holds when the predecessor's kernels were all enqueued (bank_dirty otherwise) and ran
+// on the same stream; after a failed launch or on a stream change this launch zeroes its bank itself, on
+// its own stream.  Launches on different streams are ordered by the caller (include/yfm.h: a context's
+// scratch serves one launch at a time), so no event is recorded per launch — one was, in an earlier
+// round-4 build, and cost 4.7 µs of every config-2 call (profiles/r4/exp1/) — and the library never
+// touches the previous launch's stream (the estimator destroys its group streams).  The bank index flips
+// only once the launch succeeded.  A pipelined chunk continues its batch's counters and only resets the
+// deferral list length.
 int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int B, const int* d_T_use,
            double* d_out, double* d_rb, double* d_rP, hipStream_t s, int horizon = 0, int rec_len = 0,
            const PanelView* pv = nullptr, bool reset_flags = true, yfm::Workspace* ws = nullptr) {
@@ -221,10 +220,10 @@ int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int 
   int& w_bank = ws ? ws->bank : ctx->bank;
   bool& dirty = ws ? ws->bank_dirty : ctx->bank_dirty;
   hipStream_t& last = ws ? ws->last_stream : ctx->last_stream;
-  hipEvent_t& done = ws ? ws->done_ev : ctx->done_ev;
   unsigned int* fb = static_cast<unsigned int*>(w_flags.p);
+  // the context's own (synchronous) stream after a launch on a caller's stream: that launch may still run
+  if (!ws && s == ctx->stream) YFM_HIP_CHECK(yfm::settle_foreign_launch(ctx));
   if (reset_flags && (dirty || s != last)) {
-    if (done) YFM_HIP_CHECK(hipStreamWaitEvent(s, done, 0));
     YFM_HIP_CHECK(hipMemsetAsync(fb + yfm::kFlagsPerBank * (w_bank ^ 1), 0, yfm::kFlagsPerBank * sizeof(unsigned int), s));
     dirty = false;
   }
@@ -238,8 +237,6 @@ int launch(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P, int 
     w_bank ^= 1;
     last = s;
   }
-  if (!done) YFM_HIP_CHECK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
-  YFM_HIP_CHECK(hipEventRecord(done, s));
   return YFM_OK;
 }
 
@@ -404,6 +401,13 @@ int validate_tuse(const int* T_use, int B, int T) {
 namespace yfm {
 int api_error(int code, const char* msg) { return set_error(code, "%s", msg); }
 int panel_T(const yfm_ctx* ctx) { return ctx ? ctx->T : 0; }
+
+hipError_t settle_foreign_launch(yfm_ctx* ctx) {
+  if (!ctx || !ctx->last_stream || ctx->last_stream == ctx->stream) return hipSuccess;
+  const hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess) ctx->last_stream = nullptr;  // nothing of the context is in flight any more
+  return e;
+}
 }  // namespace yfm
 
 extern "C" {
@@ -451,7 +455,6 @@ void yfm_destroy(yfm_ctx* ctx) {
     b->release();
   ctx->scratch_dd.release();
   for (DevBuf& b : ctx->gap_buf) b.release();
-  if (ctx->done_ev) (void)hipEventDestroy(ctx->done_ev);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
   delete ctx;
@@ -488,6 +491,7 @@ int yfm_get_precision(yfm_ctx* ctx) {
 
 int yfm_set_panel(yfm_ctx* ctx, const double* Y, int N, int T, const double* maturities) {
   if (int r = check_ctx(ctx)) return r;
+  YFM_HIP_CHECK(yfm::settle_foreign_launch(ctx));  // a launch on a caller's stream may still read the panel
   if (!Y || !maturities) return set_error(YFM_EINVAL, "null Y or maturities");
   if (N < 1 || T < 1) return set_error(YFM_EINVAL, "N = %d, T = %d must be >= 1", N, T);
   const int np = yfm::fixedz_np_for(N);
@@ -774,7 +778,6 @@ Workspace* workspace_create() {
 void workspace_destroy(Workspace* w) {
   if (!w) return;
   for (DevBuf* b : {&w->flags, &w->scratch, &w->scratch_dd, &w->defer, &w->scratch_fd}) b->release();
-  if (w->done_ev) (void)hipEventDestroy(w->done_ev);
   delete w;
 }
 

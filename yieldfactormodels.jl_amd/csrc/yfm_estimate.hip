@@ -237,6 +237,8 @@ extern "C" int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const
   if (!theta0 || !theta_c_out || !ll_out) return yfm::api_error(YFM_EINVAL, "null pointer argument");
   const int Tp = yfm::panel_T(ctx);
   if (Tp <= 0) return yfm::api_error(YFM_ENOPANEL, "no panel: call yfm_set_panel first");
+  // the estimator's group streams share the context's buffers with any earlier launch on a caller's stream
+  if (yfm::settle_foreign_launch(ctx) != hipSuccess) return yfm::api_error(YFM_EHIP, "device synchronisation failed");
   if (T_use)
     for (int r = 0; r < R; ++r)
       if (T_use[r] < 1 || T_use[r] > Tp) return yfm::api_error(YFM_EINVAL, "T_use outside [1, T]");

@@ -206,7 +206,7 @@ __device__ __forceinline__ void propagate_cov_freeze(const Params<M, LEAD>& p, c
 // complex, monotone or oscillating convergence).  From A … A⁴ by sub-multiplicativity:
 // C ≤ (‖A‖² + ‖A²‖² + ‖A³‖² + ‖A⁴‖²)/(1 − ‖A⁴‖²); +Inf when ‖A⁴‖_∞ ≥ 1 (no bound: never frozen early).
 // Row j of A^k is (A')^k e_j, A'v = S⁻¹(R(Φ'v)): no M×M temporaries beyond the factors of S (the
-// GNS5 kernel has no registers for A and its powers), rolled loops (two M-vectors live).
+// GNS5 kernel has no registers for A and its powers; M ≤ 3 runs the M start vectors side by side).
 template <int M, int LEAD>
 __device__ __forceinline__ double contraction_bound(const Params<M, LEAD>& p, const double (&R)[M][M],
                                                     const double (&Pm)[M][M]) {
@@ -217,39 +217,60 @@ __device__ __forceinline__ double contraction_bound(const Params<M, LEAD>& p, co
     for (int j = 0; j <= i; ++j) S[i][j] = Pm[i][j] + R[i][j];
   LDLT<M> f;
   (void)f.factor(S);
-  double n0 = 0.0, n1 = 0.0, n2 = 0.0, n3 = 0.0;  // ‖A^k‖_∞, k = 1..4
+  double n[4] = {0.0, 0.0, 0.0, 0.0};  // ‖A^k‖_∞, k = 1..4
+  // one row of A^k per start vector e_j: v ← S⁻¹R Φ'v, ‖A^k‖_∞ = max_j Σ_i |v_i|
+  auto power_step = [&](double (&v)[M]) {
+    double w[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      double s = 0.0;
+#pragma unroll
+      for (int l = 0; l < M; ++l) s = fma(p.Phi[l][i], v[l], s);  // Φ'v
+      w[i] = s;
+    }
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      double s = 0.0;
+#pragma unroll
+      for (int l = 0; l < M; ++l) s = fma(R[i][l], w[l], s);  // R Φ'v
+      v[i] = s;
+    }
+    f.solve(v);  // S⁻¹ R Φ'v
+    double sum = 0.0;
+#pragma unroll
+    for (int i = 0; i < M; ++i) sum += fabs(v[i]);
+    return sum;
+  };
+  if constexpr (M <= 3) {
+    // the M start vectors side by side: M independent chains per power (the rolled form below is one
+    // serial chain of 4M solves, ≈ 3 µs of a config-2 launch; profiles/r4/exp1/)
+    double V[M][M];
+#pragma unroll
+    for (int j = 0; j < M; ++j)
+#pragma unroll
+      for (int i = 0; i < M; ++i) V[j][i] = (i == j) ? 1.0 : 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int j = 0; j < M; ++j) n[k] = fmax(n[k], power_step(V[j]));
+  } else {
+    // (GNS5: one column and one power at a time keeps the temporaries to two M-vectors)
 #pragma unroll 1
-  for (int j = 0; j < M; ++j) {
-    double v[M];
+    for (int j = 0; j < M; ++j) {
+      double v[M];
 #pragma unroll
-    for (int i = 0; i < M; ++i) v[i] = (i == j) ? 1.0 : 0.0;
+      for (int i = 0; i < M; ++i) v[i] = (i == j) ? 1.0 : 0.0;
 #pragma unroll 1
-    for (int k = 0; k < 4; ++k) {
-      double w[M];
-#pragma unroll
-      for (int i = 0; i < M; ++i) {
-        double s = 0.0;
-#pragma unroll
-        for (int l = 0; l < M; ++l) s = fma(p.Phi[l][i], v[l], s);  // Φ'v
-        w[i] = s;
+      for (int k = 0; k < 4; ++k) {
+        const double sum = power_step(v);
+        n[0] = (k == 0) ? fmax(n[0], sum) : n[0];
+        n[1] = (k == 1) ? fmax(n[1], sum) : n[1];
+        n[2] = (k == 2) ? fmax(n[2], sum) : n[2];
+        n[3] = (k == 3) ? fmax(n[3], sum) : n[3];
       }
-      double sum = 0.0;
-#pragma unroll
-      for (int i = 0; i < M; ++i) {
-        double s = 0.0;
-#pragma unroll
-        for (int l = 0; l < M; ++l) s = fma(R[i][l], w[l], s);  // R Φ'v
-        v[i] = s;
-      }
-      f.solve(v);  // S⁻¹ R Φ'v
-#pragma unroll
-      for (int i = 0; i < M; ++i) sum += fabs(v[i]);
-      n0 = (k == 0) ? fmax(n0, sum) : n0;
-      n1 = (k == 1) ? fmax(n1, sum) : n1;
-      n2 = (k == 2) ? fmax(n2, sum) : n2;
-      n3 = (k == 3) ? fmax(n3, sum) : n3;
     }
   }
+  const double n0 = n[0], n1 = n[1], n2 = n[2], n3 = n[3];
   const double q = n3 * n3;
   // rounding of the bound itself: a few ulps; the 1.01 margin covers it
   return (q < 1.0) ? 1.01 * (n0 * n0 + n1 * n1 + n2 * n2 + q) / (1.0 - q) : __builtin_inf();
@@ -295,6 +316,23 @@ struct FixedZFilter {
   bool wave_frozen = false;  // wave-uniform at every block boundary (wave_freeze)
   LDLT<M> fs;                // factors of S = P + R at the frozen P (valid while wave_frozen)
   double dets = 0.0;
+  // A frozen lane's det S is the same number at every data step (the same S, factorised by the same
+  // code), so its log-det terms are counted instead of multiplied into `ld` one by one: nfz frozen data
+  // steps of det fzdet since the freeze, folded into fzlog (Σ n·log|det|) when the lane thaws and at the
+  // end.  Every frozen data step counts, whichever loop (steady or full) ran it, so the loglik stays
+  // independent of the batch; the steady loop adds its block's steps in one go (count_steady).
+  int nfz = 0;
+  double fzdet = 1.0, fzlog = 0.0;
+  __device__ __forceinline__ void count_frozen(double det) {
+    fzdet = nfz == 0 ? det : fzdet;
+    ++nfz;
+  }
+  __device__ __forceinline__ void fold_frozen() {
+    fzlog += nfz == 0 ? 0.0 : (double)nfz * log(fabs(fzdet));
+    neg = neg || (nfz != 0 && fzdet < 0.0);
+    nfz = 0;
+  }
+  __device__ __forceinline__ void count_steady(int steps) { nfz += steps; }
 
   // the freeze test after a data step that moved P by (dmax, nmax); Pm holds the new P
   __device__ __forceinline__ void freeze_test(double dmax, double nmax) {
@@ -312,6 +350,7 @@ struct FixedZFilter {
   }
   // a prediction-only step moves P: the lane thaws (and clears the wave's state at the block's vote)
   __device__ __forceinline__ void thaw() {
+    fold_frozen();
     frozen = false;
     wave_frozen = false;
   }
@@ -330,11 +369,13 @@ struct FixedZFilter {
 #pragma unroll
           for (int j = 0; j <= i; ++j) S[i][j] = Pm[i][j] + R[i][j];
         dets = fs.factor(S);
+        fzdet = nfz == 0 ? dets : fzdet;  // a lane whose first frozen data step is a steady one
       }
       wave_frozen = true;
     }
   }
-  // one data step of a frozen wave: the mean update of collapsed_update with the cached factors
+  // one data step of a frozen wave: the mean update of collapsed_update with the cached factors (its
+  // log-det term is counted by the caller's count_steady)
   __device__ __forceinline__ void steady_step(const double (&zc)[M - 1], double2 yb_c) {
     double bf[M], q, det;
     if constexpr (kCacheFactors) {
@@ -353,9 +394,8 @@ struct FixedZFilter {
     propagate_mean_f<M>([&](int i, int j) { return p.Phi[i][j]; }, p.delta, bf, beta);
     last_det = det;
     last_q = q;
-    ld.mul(det);
+    if constexpr (!kCacheFactors) fzdet = nfz == 0 ? det : fzdet;  // (M = 5 refactors S: the same bits)
     sumq += q;
-    neg = neg || (det < 0.0);
   }
 
   // G = Z'Z → R, log det G, collapsed or deferred; then initialize_filter.
@@ -419,18 +459,25 @@ struct FixedZFilter {
       update(zc, yb_c, bf, Pf, det, q);
       // (a singular F at t ≥ 2 makes the loglik −Inf whatever the state; trajectories skip the update)
       if constexpr (STEADY) {
+        // (the log-det term first: `frozen` as it stood for this step's S)
+        if (frozen) {
+          count_frozen(det);
+        } else {
+          ld.mul(det);
+          neg = neg || (det < 0.0);
+        }
         propagate_mean_f<M>([&](int i, int j) { return p.Phi[i][j]; }, p.delta, bf, beta);
         double dmax, nmax;
         propagate_cov_freeze<M, LEAD>(p, Pf, Pm, frozen, dmax, nmax);
         freeze_test(dmax, nmax);
-      } else if (!RECORD || det != 0.0) {
-        propagate_state<M, LEAD>(p, bf, Pf, beta, Pm);
+      } else {
+        if (!RECORD || det != 0.0) propagate_state<M, LEAD>(p, bf, Pf, beta, Pm);
+        ld.mul(det);
+        neg = neg || (det < 0.0);
       }
       last_det = det;
       last_q = q;
-      ld.mul(det);
       sumq += q;
-      neg = neg || (det < 0.0);
 #ifdef YFM_DEBUG_LANE
       if (blockIdx.x == 0 && threadIdx.x < YFM_DEBUG_LANE)
         printf("dbg L%d t %d fast det %.17g q %.17g P00 %.17g P44 %.17g b0 %.17g z0 %.17g\n", (int)threadIdx.x, t, det, q, Pm[0][0],
@@ -470,6 +517,7 @@ struct FixedZFilter {
     double Pf[M][M];
     update(zc, yb_c, bf, Pf, det, q);
     const bool upd = det != 0.0;  // inv(F) threw: return without the update (filter.jl:151-154)
+    const bool was_frozen = frozen;
     if constexpr (STEADY) {
       if (upd) {
         propagate_mean_f<M>([&](int i, int j) { return p.Phi[i][j]; }, p.delta, bf, beta);
@@ -483,9 +531,13 @@ struct FixedZFilter {
     last_det = det;
     last_q = upd ? q : __builtin_nan("");
     if (acc) {
-      ld.mul(det);
+      if (STEADY && was_frozen) {
+        count_frozen(det);
+      } else {
+        ld.mul(det);
+        neg = neg || (det < 0.0);
+      }
       sumq += last_q;
-      neg = neg || (det < 0.0);
     }
 #ifdef YFM_DEBUG_LANE  // diagnostic builds only (tools/dbg_variants.sh)
     if (blockIdx.x == 0 && threadIdx.x < YFM_DEBUG_LANE)
@@ -523,9 +575,12 @@ struct FixedZFilter {
         ll = 0.0;
       } else {
         const double per_term = (double)(N - M) * log(sigma2) + logdetG + (double)N * kLog2Pi;
-        ll = -0.5 * ((double)nterms * per_term + ld.log_value() + sumq);
+        double lf = 0.0;  // the frozen steps' log-det terms (STEADY)
+        if constexpr (STEADY) lf = fzlog + (nfz == 0 ? 0.0 : (double)nfz * log(fabs(fzdet)));
+        ll = -0.5 * ((double)nterms * per_term + (ld.log_value() + lf) + sumq);
       }
-      if (neg || !isfinite(ll)) {  // DomainError / non-finite → -Inf (filter.jl:197-204)
+      const bool fneg = STEADY && nfz != 0 && fzdet < 0.0;
+      if (neg || fneg || !isfinite(ll)) {  // DomainError / non-finite → -Inf (filter.jl:197-204)
         ll = -__builtin_inf();
         atomicAdd(&flags[1], 1u);
       }

@@ -103,6 +103,9 @@ int loglik_device_ws(yfm_ctx* ctx, Workspace* ws, int kind, int space, const dou
 int api_error(int code, const char* msg);
 // columns of the context's panel (0 before yfm_set_panel)
 int panel_T(const yfm_ctx* ctx);
+// a synchronous entry point about to use the context after an asynchronous launch on a caller's stream:
+// wait for the device (the caller's stream may be gone, so it is never waited on by handle)
+hipError_t settle_foreign_launch(yfm_ctx* ctx);
 hipError_t launch_prep_panel(const double* Y, int N, int T, int np, int ldp, double* out, hipStream_t s);
 
 }  // namespace yfm

@@ -577,6 +577,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
           // basic block — a branch inside would let the compiler sink the arithmetic below the MFMAs
           rotate(t0 + TB - 1);
           steady_steps += TB;
+          f.count_steady(TB);
           have_next = true;
         }
       }
@@ -598,6 +599,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
           }
           if (tt < tend) shalf(tt, zc, yb, zn, ybn);
           steady_steps += tend;
+          f.count_steady(tend);
         }
       }
       if (!blk_steady) {
@@ -606,7 +608,9 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
           half(tt, zc, yb, meta, zn, ybn, metan);
           half(tt + 1, zn, ybn, metan, zc, yb, meta);
           if constexpr (STEADY) {
-            if (tt == TB / 2 - 2) f.prepare_bound();  // mid-block as well: lanes may freeze within this block
+            // mid-block as well: lanes may freeze within this block (without it the config-2 steady share
+            // drops 0.973 → 0.947, 0.226 → 0.234 ms; profiles/r4/exp1/)
+            if (tt == TB / 2 - 2) f.prepare_bound();
           }
         }
         if (tt < tend) half(tt, zc, yb, meta, zn, ybn, metan);
@@ -680,10 +684,13 @@ static int gns5_steady_enabled() {
   return (e && e[0] == '1') ? 1 : 0;
 }
 
-// the pipelined steady blocks of the DNS kernel (PIPE): on unless YFM_DNS_PIPE=0
+// the pipelined steady blocks of the DNS kernel (PIPE): off unless YFM_DNS_PIPE=1.  FP64 MFMA and FP64
+// VALU share one pipe on gfx950 (tools/mfma_valu_overlap.hip: one MFMA wave + one VALU wave per SIMD take
+// the sum of their times), so the overlap can only fill latency bubbles: measured 0.2230 vs 0.2196 ms
+// without it on the final build (profiles/r4/exp2/)
 static int pipe_enabled() {
   const char* e = std::getenv("YFM_DNS_PIPE");
-  return (e && e[0] == '0') ? 0 : 1;
+  return (e && e[0] == '1') ? 1 : 0;
 }
 
 // diagnostic: YFM_FZ_SPLIT_FORM=1 selects the two-function update form (FixedZFilter SPLIT_FORM)
@@ -715,7 +722,7 @@ static hipError_t launch_fixedz_np(const LaunchArgs& a) {
     const bool on = steady_enabled() && a.T >= kSteadyMinT && (M != 5 || gns5_steady_enabled());
     auto* k = (kSteady && on) ? &fixedz_loglik_kernel<NP, M, LEAD, false, kSteady>
                               : &fixedz_loglik_kernel<NP, M, LEAD, false, false>;
-    // DNS: the steady blocks overlap the next block's Z'ỹ MFMAs with their mean updates (YFM_DNS_PIPE=0: off)
+    // DNS: the steady blocks overlap the next block's Z'ỹ MFMAs with their mean updates (YFM_DNS_PIPE=1: on)
     if constexpr (kSteady && M == 3) {
       if (k == &fixedz_loglik_kernel<NP, M, LEAD, false, kSteady> && pipe_enabled())
         k = &fixedz_loglik_kernel<NP, M, LEAD, false, kSteady, false, true>;

@@ -342,24 +342,12 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         double z = (j < N) ? exp(-(lam * s_mr[j].x)) : 0.0;
-        // operands one maturity ahead, the jump index two ahead (as yfm_tvl_dd.hip: an LDS round trip
-        // per maturity would otherwise wait twice per trip); indices past the lane's last maturity are
-        // clamped to N − 1 (read, never used)
-        const int i0 = min(j, N - 1);
-        double2 mr_c = s_mr[i0];
-        double y_c = col[i0], wn_c = w[s_gi[i0]];
-        int g_n = s_gi[min(j + L, N - 1)];
+#pragma unroll 2
         for (int i = j; i < N; i += L) {
-          const int in = min(i + L, N - 1);
-          double2 mr_n = s_mr[in];
-          double y_n = col[in], wn_n = w[g_n];
-          g_n = s_gi[min(i + 2 * L, N - 1)];
-          accum(mr_c, z, y_c);
-          z *= wn_c;
-          asm volatile("" : "+v"(mr_n.x), "+v"(mr_n.y), "+v"(y_n), "+v"(wn_n), "+v"(g_n));
-          mr_c = mr_n;
-          y_c = y_n;
-          wn_c = wn_n;
+          const double2 mr = s_mr[i];
+          const double wn = w[s_gi[i]];
+          accum(mr, z, col[i]);
+          z *= wn;
         }
       } else {
 #pragma unroll 2

@@ -473,7 +473,10 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
       const double sgzz = split_const(l_n * Be * Be);
       const double sy2 = split_const(By * Bz2), syz = split_const(By * Be);
       dd_acc S2, Sz, S4, G22, G2z, G24, Gzz, Gz4, G44, Y2, Yz, Y4;
-      auto accum = [&](double m, double y, dd rm, dd z) {
+      auto accum = [&](int i, dd z) {
+        const double m = s_m[i];
+        const double y = col[i];
+        const dd rm = s_rm[i];
         const dd it = dd_mul_nn(rl, rm);  // 1/τ
         // 1 − z exactly (Fast2Sum: 1 ≥ z.hi), then (1 − z)/τ
         const double o1 = 1.0 - z.hi;
@@ -526,32 +529,13 @@ __global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // The operands of maturity i are loaded one maturity ahead and its jump index two ahead: at one
-        // wave per SIMD an LDS round trip per maturity would otherwise stall the loop twice (the jump
-        // index, then the jump factor it selects).  Indices past the lane's last maturity are clamped to
-        // N − 1 (read, never used).
-        const int i0 = min(j, N - 1), i1 = min(j + L, N - 1);
-        double m_c = s_m[i0], y_c = col[i0];
-        dd rm_c = s_rm[i0], wn_c = w[s_gi[i0]];
-        int g_n = s_gi[i1];
         for (int i = j; i < N; i += L) {
-          const int in = min(i + L, N - 1);
-          double m_n = s_m[in], y_n = col[in];
-          dd rm_n = s_rm[in], wn_n = w[g_n];
-          g_n = s_gi[min(i + 2 * L, N - 1)];
-          accum(m_c, y_c, rm_c, z);
-          z = dd_mul(z, wn_c);
-          // the next maturity's operands pass through here, at the end of this one: the optimiser cannot
-          // fold their loads back into the next trip (where they would wait on the LDS at once)
-          asm volatile("" : "+v"(m_n), "+v"(y_n), "+v"(g_n));
-          asm volatile("" : "+v"(rm_n.hi), "+v"(rm_n.lo), "+v"(wn_n.hi), "+v"(wn_n.lo));
-          m_c = m_n;
-          y_c = y_n;
-          rm_c = rm_n;
-          wn_c = wn_n;
+          const dd wn = w[s_gi[i]];
+          accum(i, z);
+          z = dd_mul(z, wn);
         }
       } else {
-        for (int i = j; i < N; i += L) accum(s_m[i], col[i], s_rm[i], dd_exp(neg_rate(lam, s_m[i])));
+        for (int i = j; i < N; i += L) accum(i, dd_exp(neg_rate(lam, s_m[i])));
       }
       const dd s2 = group_sum_acc<L>(S2), sz = group_sum_acc<L>(Sz), s4 = group_sum_acc<L>(S4);
       const dd g22 = group_sum_acc<L>(G22), g2z = group_sum_acc<L>(G2z), g24 = group_sum_acc<L>(G24);
