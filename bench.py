@@ -340,10 +340,25 @@ def pmc_traffic(kernel_substr: str, evals: int):
     return None, None
 
 
-DOMINANT = {KIND_DNS: "fixedz_loglik_kernel<30, 3, 1, false, true>", KIND_GNS: "fixedz_loglik_kernel<30, 5, 2, false, true>",
-            (KIND_DNS, "full"): "fixedz_loglik_kernel<30, 3, 1, false, false>",
-            (KIND_GNS, "full"): "fixedz_loglik_kernel<30, 5, 2, false, false>",
+# the instantiation each configuration runs: fixedz_loglik_kernel<NP, M, LEAD, RECORD, STEADY, SPLIT_FORM, PIPE>
+# (DNS: frozen-covariance steady state by default; GNS5: full recursion unless YFM_GNS5_STEADY=1)
+DOMINANT = {(KIND_DNS, "steady"): "fixedz_loglik_kernel<30, 3, 1, false, true, false, false>",
+            (KIND_DNS, "pipe"): "fixedz_loglik_kernel<30, 3, 1, false, true, false, true>",
+            (KIND_DNS, "full"): "fixedz_loglik_kernel<30, 3, 1, false, false, false, false>",
+            (KIND_GNS, "steady"): "fixedz_loglik_kernel<30, 5, 2, false, true, false, false>",
+            (KIND_GNS, "full"): "fixedz_loglik_kernel<30, 5, 2, false, false, false, false>",
             (KIND_TVL, "fp64"): "tvl_loglik_kernel", (KIND_TVL, "certified"): "tvl_dd_loglik_kernel"}
+
+
+def dominant_kernel(kind, prec):
+    env = os.environ.get
+    if kind == KIND_TVL:
+        return DOMINANT[(kind, prec)]
+    if env("YFM_DNS_STEADY", "1").startswith("0"):
+        return DOMINANT[(kind, "full")]
+    if kind == KIND_GNS:
+        return DOMINANT[(kind, "steady" if env("YFM_GNS5_STEADY", "0").startswith("1") else "full")]
+    return DOMINANT[(kind, "pipe" if env("YFM_DNS_PIPE", "0").startswith("1") else "steady")]
 
 
 def roofline(kind, prec, N, M, T, T_use, B, P, kernel_ms, steady_lane_steps=0):
@@ -356,12 +371,7 @@ def roofline(kind, prec, N, M, T, T_use, B, P, kernel_ms, steady_lane_steps=0):
     f_rank -= steady_lane_steps * (collapsed_update_flops(M) - steady_update_flops(M))
     f_survey = float(np.sum(alg_flops(kind, N, M, Tb, survey_flops_step)))
     achieved = f_rank / (kernel_ms * 1e-3) / 1e12
-    if kind == KIND_TVL:
-        name = DOMINANT[(kind, prec)]
-    elif kind in (KIND_DNS, KIND_GNS) and os.environ.get("YFM_DNS_STEADY", "1").startswith("0"):
-        name = DOMINANT[(kind, "full")]  # the full-recursion instantiation
-    else:
-        name = DOMINANT[kind]
+    name = dominant_kernel(kind, prec)
     traffic, traffic_src = pmc_traffic(name, B)
     exe = pmc_executed_flops(name, B)
     steps = float(np.sum(Tb - 1))

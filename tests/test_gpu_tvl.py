@@ -162,7 +162,8 @@ def test_tvl_config3_1024_certified(engine, config3_1024):
     e = rel(got, fx["loglik_truth"])
     print("certified 1024", table, "max rel vs truth %.2e, %d above 1e-13" % (e.max(), (e > EXACT).sum()))
     assert table["failing"] == 0
-    assert e.max() <= 1e-9 and (e > EXACT).sum() <= 10
+    # the measured count (5 on every build since round 3: profiles/r3/tvl_dd_ab*, profiles/r4/ab2, ab3)
+    assert e.max() <= 1e-9 and (e > EXACT).sum() <= 5
 
 
 def test_tvl_config3_1024_fp64_reference_class(engine, config3_1024):

@@ -152,10 +152,9 @@ __device__ __forceinline__ double split_const(double x) {
   return __builtin_ldexp(1.0, __builtin_amdgcn_frexp_exp(x));
 }
 
-// exp of a dd argument to ~2u² relative: x = k·ln2 + r, |r| ≤ ln2/2, e^r from a degree-14
-// Taylor polynomial of r/2^4 followed by 4 squarings of (1 + s) carried as s ← s(2 + s).
+// exp of a dd argument to ~2u² relative: x = k·ln2 + r, |r| ≤ ln2/2, e^r from a degree-9
+// Taylor polynomial of r/2^9 followed by 9 squarings of (1 + s) carried as s ← s(2 + s).
 // Arguments beyond the FP64 range give 0 / Inf like exp(); NaN propagates.
-constexpr int kExpSquarings = 4;
 __device__ __forceinline__ dd dd_exp(dd x) {
   constexpr double kLn2Hi = 0.6931471805599453094172321214581766;  // nearest double to ln 2
   constexpr double kLn2Lo = 2.3190468138462996154e-17;             // ln 2 − kLn2Hi
@@ -166,11 +165,9 @@ __device__ __forceinline__ dd dd_exp(dd x) {
   const dd kh = two_prod(k, kLn2Hi);
   dd r = dd_sub(x, kh);
   r = dd_add_d(r, -k * kLn2Lo);
-  r = dd_ldexp(r, -kExpSquarings);
-  // s = e^r − 1 = r + r²/2! + … + r^14/14!  (Horner on 1/n!), |r| ≤ ln2/2⁵ = 0.0217: the terms n ≥ 9
-  // (≤ 2.7e-21 of e^r − 1) carry no bit of a dd result beyond FP64, so their Horner runs in FP64 on r.hi
-  // and only n ≤ 8 in dd; 4 squarings instead of 9 (round 3: degree 9 on r/2⁹, all dd)
-  constexpr double inv_fact[15] = {1.0,
+  r = dd_ldexp(r, -9);
+  // s = e^r − 1 = r + r²/2! + … + r⁹/9!  (Horner on 1/n!)
+  constexpr double inv_fact[10] = {1.0,
                                    1.0,
                                    0.5,
                                    1.6666666666666666574e-01,
@@ -179,30 +176,23 @@ __device__ __forceinline__ dd dd_exp(dd x) {
                                    1.3888888888888889419e-03,
                                    1.9841269841269841253e-04,
                                    2.4801587301587301566e-05,
-                                   2.7557319223985892511e-06,
-                                   2.7557319223985888276e-07,
-                                   2.5052108385441720224e-08,
-                                   2.0876756987868100187e-09,
-                                   1.6059043836821613341e-10,
-                                   1.1470745597729724507e-11};
-  constexpr double inv_fact_lo[9] = {0.0,
-                                     0.0,
-                                     0.0,
-                                     9.2518585385429706566e-18,
-                                     2.3129646346357426641e-18,
-                                     1.1564823173178713802e-19,
-                                     -5.3005439543735770590e-20,
-                                     1.7209558293420705286e-22,
-                                     2.1511947866775881608e-23};
-  double t = inv_fact[14];
+                                   2.7557319223985892511e-06};
+  constexpr double inv_fact_lo[10] = {0.0,
+                                      0.0,
+                                      0.0,
+                                      9.2518585385429706566e-18,
+                                      2.3129646346357426641e-18,
+                                      1.1564823173178713802e-19,
+                                      -5.3005439543735770590e-20,
+                                      1.7209558293420705286e-22,
+                                      2.1511947866775881608e-23,
+                                      -1.8583932740464720810e-22};
+  dd p = {inv_fact[9], inv_fact_lo[9]};
 #pragma unroll
-  for (int n = 13; n >= 9; --n) t = __builtin_fma(t, r.hi, inv_fact[n]);
-  dd p = dd_add(dd_mul_d(r, t), dd{inv_fact[8], inv_fact_lo[8]});
-#pragma unroll
-  for (int n = 7; n >= 1; --n) p = dd_add(dd_mul(p, r), dd{inv_fact[n], inv_fact_lo[n]});
+  for (int n = 8; n >= 1; --n) p = dd_add(dd_mul(p, r), dd{inv_fact[n], inv_fact_lo[n]});
   dd s = dd_mul(p, r);
 #pragma unroll
-  for (int i = 0; i < kExpSquarings; ++i) s = dd_mul(s, dd_add_d(s, 2.0));
+  for (int i = 0; i < 9; ++i) s = dd_mul(s, dd_add_d(s, 2.0));
   const dd e = dd_add_d(s, 1.0);
   return dd_ldexp(e, (int)k);
 }
