@@ -25,8 +25,8 @@
 // i ≡ j (mod L) and their dd loadings; per step each lane forms the innovation of its maturities
 // and its share of u = Z'v and v'v, the group reduces them with DPP / permlane butterflies
 // (dd-exact pairwise sums, every lane ends with the same bits) and every lane runs the M×M
-// update.  Decoding and initialize_filter run in dd in fixedz_dd_init_kernel (one thread per
-// deferred candidate) and hand over a per-candidate record.  Deferred lanes are rare (none in the
+// update.  Decoding and initialize_filter run in dd in fd_init_record (one lane per deferred
+// candidate, at the top of its slot) and hand over a per-candidate record.  Deferred lanes are rare (none in the
 // benchmark configurations), so the kernels read the deferral list the FP64 kernel
 // built on the device and launch one filter slot per candidate of the batch, the slots past the
 // list exiting at once.
@@ -43,7 +43,7 @@ namespace {
 constexpr int kFdBlock = 256;
 constexpr int kFdPre = 8;  // panel doubles prefetched per thread per chunk
 
-// per-candidate record written by fixedz_dd_init_kernel (doubles), parametrised by M
+// per-candidate record written by fd_init_record (doubles), parametrised by M
 template <int M>
 struct FdRec {
   static constexpr int U = M * (M + 1) / 2;  // upper-triangle entries
@@ -106,18 +106,16 @@ __device__ __forceinline__ void fd_propagate(const double* par, const dd (&b)[M]
 
 }  // namespace
 
-// decode θ_b in dd (transform_params + set_params!) and run initialize_filter (filter.jl:1-10) for
-// deferred slot g (candidate defer_list[g])
+// decode θ_b in dd (transform_params + set_params!) and run initialize_filter (filter.jl:1-10) into the
+// record r of one deferred candidate.  Called by one lane of the candidate's group inside
+// fixedz_dd_loglik_kernel (round 4: a separate init kernel cost a ~4.4 µs launch on every config-2 call,
+// deferred lanes or not); not inlined, so its ~6×6 / 15×15 dd solves do not shape the filter's registers.
 template <int M, int LEAD>
-__global__ __launch_bounds__(64) void fixedz_dd_init_kernel(const double* __restrict__ theta, int P, int space,
-                                                            const int* __restrict__ defer_list,
-                                                            const int* __restrict__ defer_count,
-                                                            double* __restrict__ rec) {
+__device__ __noinline__ void fd_init_record(const double* __restrict__ theta, int P, int space, int b,
+                                            double* __restrict__ r) {
   using R = FdRec<M>;
-  const int nd = *defer_count;
-  for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < nd; g += gridDim.x * blockDim.x) {
-  const double* th = theta + (size_t)defer_list[g] * P + LEAD;
-  double* r = rec + (size_t)g * R::Len;
+  {
+  const double* th = theta + (size_t)b * P + LEAD;
   int k = 0;
   const dd sig2 = space == 0 ? dd_exp(dd_make(th[k])) : dd_make(th[k]);
   ++k;
@@ -213,8 +211,8 @@ __global__ __launch_bounds__(64) void fixedz_dd_init_kernel(const double* __rest
 
 template <int L, int M, int LEAD, bool RECORD>
 __global__ __launch_bounds__(kFdBlock) void fixedz_dd_loglik_kernel(
-    const double* __restrict__ rec, const int* __restrict__ defer_list, const int* __restrict__ defer_count,
-    const double* __restrict__ theta, int P, const double* __restrict__ Y, const double* __restrict__ prep, int ldp,
+    double* __restrict__ rec, const int* __restrict__ defer_list, const int* __restrict__ defer_count,
+    const double* __restrict__ theta, int P, int space, const double* __restrict__ Y, const double* __restrict__ prep, int ldp,
     int np, int T, int N, int TC, const double* __restrict__ mats, const int* __restrict__ T_use,
     double* __restrict__ out, unsigned int* __restrict__ flags, double* __restrict__ rec_beta,
     double* __restrict__ rec_P, int horizon, int rec_len) {
@@ -243,6 +241,8 @@ __global__ __launch_bounds__(kFdBlock) void fixedz_dd_loglik_kernel(
   const int nobs = T_use ? T_use[b] : T;
 
   if (tid == 0) s_nobs_max = 0;
+  if (live && j == 0) fd_init_record<M, LEAD>(theta, P, space, b, rec + (size_t)gg * R::Len);
+  __syncthreads();  // the record (global memory, this workgroup) before its lanes read it
   const double* r = rec + (size_t)gg * R::Len;
   double* par = s_par + grp * R::Par;
   for (int q = j; q < R::Par; q += L) par[q] = r[q];
@@ -484,18 +484,18 @@ __global__ __launch_bounds__(kFdBlock) void fixedz_dd_loglik_kernel(
 namespace {
 
 template <int L, int M, int LEAD>
-hipError_t launch_fd_l(const LaunchArgs& a, const double* rec, int TC) {
+hipError_t launch_fd_l(const LaunchArgs& a, double* rec, int TC) {
   constexpr int GPB = kFdBlock / L;
   const int grid = std::min((a.B + GPB - 1) / GPB, 256);
   const size_t shmem = sizeof(double) * ((size_t)TC + (size_t)TC * a.N + (size_t)GPB * FdRec<M>::Par);
   if (shmem > 64 * 1024) return hipErrorInvalidValue;
   if (a.rec_beta) {
     hipLaunchKernelGGL((fixedz_dd_loglik_kernel<L, M, LEAD, true>), dim3(grid), dim3(kFdBlock), shmem, a.stream, rec,
-                       a.defer_list, a.defer_count, a.theta, a.P, a.raw, a.panel, a.ldp, a.np, a.T, a.N, TC, a.mats,
+                       a.defer_list, a.defer_count, a.theta, a.P, a.space, a.raw, a.panel, a.ldp, a.np, a.T, a.N, TC, a.mats,
                        a.T_use, a.out, a.flags, a.rec_beta, a.rec_P, a.horizon, a.rec_len);
   } else {
     hipLaunchKernelGGL((fixedz_dd_loglik_kernel<L, M, LEAD, false>), dim3(grid), dim3(kFdBlock), shmem, a.stream, rec,
-                       a.defer_list, a.defer_count, a.theta, a.P, a.raw, a.panel, a.ldp, a.np, a.T, a.N, TC, a.mats,
+                       a.defer_list, a.defer_count, a.theta, a.P, a.space, a.raw, a.panel, a.ldp, a.np, a.T, a.N, TC, a.mats,
                        a.T_use, a.out, a.flags, nullptr, nullptr, 0, 0);
   }
   return hipGetLastError();
@@ -503,9 +503,6 @@ hipError_t launch_fd_l(const LaunchArgs& a, const double* rec, int TC) {
 
 template <int M, int LEAD>
 hipError_t launch_fd_m(const LaunchArgs& a, double* rec) {
-  hipLaunchKernelGGL((fixedz_dd_init_kernel<M, LEAD>), dim3(std::min((a.B + 63) / 64, 64)), dim3(64), 0, a.stream, a.theta, a.P,
-                     a.space, a.defer_list, a.defer_count, rec);
-  if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
   constexpr int MPL = M >= 5 ? 8 : 16;
   int L = 4;
   while (L * MPL < a.N && L < 64) L <<= 1;
