@@ -45,7 +45,9 @@ __device__ __forceinline__ void decode_params(const double* __restrict__ th, int
   int k = 0;
 #pragma unroll
   for (int l = 0; l < LEAD; ++l) p.gam[l] = th[k++];
-  p.sigma2 = space == 0 ? exp(th[k]) : th[k];
+  // (the exps are computed unconditionally and selected: a branch on `space` put each in its own block)
+  const double e_s = exp(th[k]);
+  p.sigma2 = space == 0 ? e_s : th[k];
   ++k;
   double U[M][M];
 #pragma unroll
@@ -54,7 +56,10 @@ __device__ __forceinline__ void decode_params(const double* __restrict__ th, int
     for (int i = 0; i < M; ++i) {
       if (i <= j) {
         double x = th[k++];
-        if (i == j && space == 0) x = exp(x);
+        if (i == j) {
+          const double e = exp(x);
+          x = space == 0 ? e : x;
+        }
         U[i][j] = x;
       } else {
         U[i][j] = 0.0;
@@ -77,7 +82,10 @@ __device__ __forceinline__ void decode_params(const double* __restrict__ th, int
 #pragma unroll
     for (int j = 0; j < M; ++j) {
       double x = th[k++];
-      if (i == j && space == 0) x = from_R_to_11(x);
+      if (i == j) {
+        const double e = from_R_to_11(x);
+        x = space == 0 ? e : x;
+      }
       p.Phi[i][j] = x;  // reshape(·, M, M)' == row-major (paramoperations.jl:38)
     }
 }

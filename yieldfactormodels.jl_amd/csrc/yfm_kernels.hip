@@ -155,7 +155,10 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   constexpr bool USE_MFMA = (NZ == 2 || NZ == 4) && (NP <= 32);  // fragments + LDS scratch budget
   constexpr int NK = (NP + 3) / 4;            // MFMA k-steps (4 maturities each)
   constexpr int NRT = 64 * NZ / 16;           // MFMA row tiles per wave (16 (cand, col) pairs each)
-  constexpr int RGN = (NZ == 2) ? NRT : 4;    // row tiles accumulated at once (bounds live accumulators)
+  // row tiles accumulated at once (bounds live accumulators).  DNS: two groups of 4, so the first group's
+  // z̃ stores overlap the second group's MFMAs (8: 0.2173 → 4: 0.2165 ms at config 2, 2: 0.2197 ms — two
+  // accumulator chains expose the MFMA latency; profiles/r4/ab9, ab10)
+  constexpr int RGN = 4;
   constexpr int RGN4 = (NZ == 2) ? NRT : 8;   // the same for the 4×4×4 form (one double per accumulator)
   constexpr int TB = 16;                      // steps per MFMA block
   // GNS5 (two γ): the MFMA rows are e_l = 1 − e^{−λ_l m} (one per γ) against the panel columns ỹ and
@@ -166,7 +169,8 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   constexpr int RPC = ZB ? LEAD : NZ;         // fragment rows per candidate
   constexpr int NRTA = 64 * RPC / 16;         // fragment row tiles per wave
   constexpr int SS = 64 * NZ + 2;             // scratch row stride (doubles): one row per step
-  constexpr int SCR = USE_MFMA ? (TB * SS) : 2;
+  // (also the fragment staging image of 32 candidates: 32·RPC rows of 4·NK + 1 maturities)
+  constexpr int SCR = USE_MFMA ? ((TB * SS > 32 * RPC * (4 * NK + 1)) ? TB * SS : 32 * RPC * (4 * NK + 1)) : 2;
   // PIPE (DNS steady state): a steady block issues the NEXT block's Z'ỹ MFMAs between its own mean
   // updates — the matrix pipe and the VALU then work side by side instead of one after the other — into
   // a second scratch buffer per wave (2 × 16.6 KB per wave: 151.5 KB of LDS at NP = 32)
@@ -180,6 +184,9 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   __shared__ int s_nobs_max;
   __shared__ double s_rm[ZB ? NP : 1];  // 1/m_i (0 past N)
 
+#ifdef YFM_PHASE_PROBE  // timing probe builds only (tools/phase_run.py): per-wave cycles by phase, printf'd
+  const long long ph_entry = __builtin_readcyclecounter();
+#endif
   if (flags_next && blockIdx.x == 0 && threadIdx.x < kFlagsPerBank) flags_next[threadIdx.x] = 0u;  // the next launch's counters
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -202,8 +209,38 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   atomicMax(&s_nobs_max, live ? my_steps : 0);
 
   // ---- decode θ_b, loadings, Z'Z, initial state ----------------------------------
+  // The wave's 64 θ rows are contiguous (64·P doubles): staged through the wave's scratch with coalesced
+  // loads (a lane reading its own row directly touches one cache line per lane and parameter), then each
+  // lane decodes its row from LDS.  Needs the model's own parameter count and room in the scratch.
+  constexpr int kP = param_count(M, LEAD);
+  const double* th_row = theta + (size_t)bb * P;
+  if constexpr (USE_MFMA && 64 * kP <= SCR) {
+    if (P == kP) {
+      const int w0 = min(blockIdx.x * kBlock + wave * 64, B - 1);  // first row of this wave's range
+      const int n = min(64, B - w0) * kP;
+      const double* src = theta + (size_t)w0 * kP;
+      double* thl = scratch[wave][0];
+      double v[kP];
+#pragma unroll
+      for (int r = 0; r < kP; ++r) {
+        const int e = r * 64 + lane;
+        v[r] = (e < n) ? src[e] : 0.0;
+      }
+#pragma unroll
+      for (int r = 0; r < kP; ++r) thl[r * 64 + lane] = v[r];
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's own rows
+      __builtin_amdgcn_wave_barrier();
+      th_row = thl + (bb - w0) * kP;
+    }
+  }
   Params<M, LEAD> p;
-  decode_params<M, LEAD>(theta + (size_t)bb * P, space, p);
+  decode_params<M, LEAD>(th_row, space, p);
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // the rows are read before the fragment staging reuses the scratch
+  __builtin_amdgcn_wave_barrier();
+#ifdef YFM_PHASE_PROBE
+  asm volatile("" ::"v"(p.sigma2));
+  const long long ph_s1 = __builtin_readcyclecounter();
+#endif
 
   double Zc[NZ][NP];
 #pragma unroll
@@ -211,16 +248,13 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     const double lam = 1e-2 + exp(p.gam[l]);  // dns.jl:55
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
-      if (i < N) {
-        const double tau = lam * mats[i];
-        const double z = exp(-tau);
-        const double s = (1.0 - z) / tau;
-        Zc[2 * l][i] = s;
-        Zc[2 * l + 1][i] = s - z;
-      } else {
-        Zc[2 * l][i] = 0.0;
-        Zc[2 * l + 1][i] = 0.0;
-      }
+      // branch-free (maturities past N computed on a clamped index and zeroed): with `if (i < N)` every
+      // maturity was its own basic block and the 30 exp/div chains ran one after another
+      const double tau = lam * mats[max(min(i, N - 1), 0)];
+      const double z = exp(-tau);
+      const double s = (1.0 - z) / tau;
+      Zc[2 * l][i] = (i < N) ? s : 0.0;
+      Zc[2 * l + 1][i] = (i < N) ? s - z : 0.0;
     }
   }
   double G[M][M];
@@ -242,6 +276,10 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     }
   }
 
+#ifdef YFM_PHASE_PROBE
+  asm volatile("" ::"v"(G[1][2]));
+  const long long ph_s2 = __builtin_readcyclecounter();
+#endif
   // MFMA A fragments: tile r, k-step kk — lane l holds Z of pair p = 16r + (l & 15)
   // (candidate p >> 1 of this wave, column p & 1) at maturity 4kk + (l >> 4).
   // Gathered once through the wave's scratch, 16 candidates at a time.
@@ -251,19 +289,24 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   for (int l = 0; l < LEAD; ++l) rlam[l] = 1.0 / (1e-2 + exp(p.gam[l]));
   if constexpr (USE_MFMA) {
     constexpr int ZS = 4 * NK + 1;  // maturity stride of the staging image (odd: conflict-free LDS)
-    constexpr int QT = NRTA / 4;  // row tiles per quarter (16 candidates)
-    static_assert(16 * RPC * ZS <= SCR, "staging fits the scratch");
+    constexpr int HT = NRTA / 2;    // row tiles per half wave (32 candidates)
+    static_assert(32 * RPC * ZS <= SCR, "staging fits the scratch");
+    // two rounds of 32 candidates (round 3: four of 16, with a block barrier after each write and read — the
+    // scratch is the wave's own, so the wave's LDS counter and a wave barrier order it; profiles/r4/ab13)
     double* st = scratch[wave][0];
 #pragma unroll
-    for (int qu = 0; qu < 4; ++qu) {
-      if ((lane >> 4) == qu) {
-        const int cl = lane & 15;
+    for (int h = 0; h < 2; ++h) {
+      if ((lane >> 5) == h) {
+        const int cl = lane & 31;
         if constexpr (ZB) {
 #pragma unroll
           for (int l = 0; l < LEAD; ++l) {
             const double lam = 1e-2 + exp(p.gam[l]);
 #pragma unroll
-            for (int m = 0; m < ZS; ++m) st[(cl * RPC + l) * ZS + m] = (m < N) ? 1.0 - exp(-(lam * mats[m])) : 0.0;
+            for (int m = 0; m < ZS; ++m) {
+              const double e = 1.0 - exp(-(lam * mats[max(min(m, N - 1), 0)]));
+              st[(cl * RPC + l) * ZS + m] = (m < N) ? e : 0.0;
+            }
           }
         } else {
 #pragma unroll
@@ -272,17 +315,22 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
             for (int m = 0; m < ZS; ++m) st[(cl * NZ + c) * ZS + m] = (m < NP) ? Zc[c][m] : 0.0;
         }
       }
-      __syncthreads();
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int r = qu * QT; r < (qu + 1) * QT; ++r) {
-        const int pr = 16 * r + (lane & 15) - qu * 16 * RPC;  // pair index within this quarter
+      for (int r = h * HT; r < (h + 1) * HT; ++r) {
+        const int pr = 16 * r + (lane & 15) - h * 32 * RPC;  // pair index within this half
 #pragma unroll
         for (int kk = 0; kk < NK; ++kk) Af[r][kk] = st[pr * ZS + 4 * kk + (lane >> 4)];
       }
-      __syncthreads();
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
     }
   }
 
+#ifdef YFM_PHASE_PROBE
+  const long long ph_s3 = __builtin_readcyclecounter();
+#endif
   FixedZFilter<M, LEAD, RECORD, STEADY, SPLIT_FORM> f;
   f.p = p;
   f.steady_ok = steady != 0;
@@ -301,6 +349,10 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
       }
     f.init_ok = init_rec[(size_t)q * B + bb] != 0.0;
   }
+#ifdef YFM_PHASE_PROBE
+  asm volatile("" ::"v"(f.Pm[0][1]), "v"(f.R[0][1]));
+  const long long ph_s4 = __builtin_readcyclecounter();
+#endif
   // ill-conditioned Z'Z: this candidate is evaluated by the double-double capacitance kernel
   // instead (yfm_fixedz_dd.hip); its lane here runs along without writing
   const bool defer = live && !f.collapsed;
@@ -365,6 +417,10 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     }
   };
 
+#ifdef YFM_PHASE_PROBE
+  long long ph_t0 = __builtin_readcyclecounter(), ph_bound = 0, ph_bload = 0, ph_mfma = 0, ph_dec = 0, ph_st = 0, ph_full = 0;
+  int ph_nst = 0, ph_nfull = 0;
+#endif
   if constexpr (USE_MFMA) {
     unsigned int steady_steps = 0;  // STEADY: this wave's steady steps (one atomic at the end: a per-block
                                     // atomic would put its latency on the next global load's wait)
@@ -373,10 +429,19 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     for (int t0 = 0; t0 < nsteps; t0 += TB) {
       // the freeze rule's contraction bound, once per lane, at a block boundary before the block's MFMA
       // accumulators are live (FixedZFilter::prepare_bound)
+#ifdef YFM_PHASE_PROBE
+      const long long ph_a = __builtin_readcyclecounter();
+#endif
       if constexpr (STEADY) f.prepare_bound();
+#ifdef YFM_PHASE_PROBE
+      long long ph_a2 = __builtin_readcyclecounter(), ph_a3 = ph_a2;
+#endif
       double* scr = scratch[wave][PIPE ? buf : 0];
       // ---- z̃ for steps t0 .. t0+15 of all 64 candidates: NRT·NK MFMAs ----
       const double* cb = col_of(t0);  // TB consecutive columns of one chunk
+      // the block's NaN flags, one column per lane, read before the MFMAs so the steady-block vote after them
+      // does not wait for an LDS round trip (0.2179 → 0.2168 ms at config 2, profiles/r4/ab9/)
+      const double col_flag = cb[min(lane, TB - 1) * LDP + NP + 2];
       if (have_z) {
         // (PIPE) already in scratch[wave][buf]
       } else if constexpr (ZB) {
@@ -448,6 +513,10 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
           const int m = 4 * kk + (lane >> 4);
           bvk[kk] = (m < NP) ? cb[(lane & 15) * LDP + m] : 0.0;  // B[k = m][col = step]
         }
+#ifdef YFM_PHASE_PROBE
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        ph_a3 = __builtin_readcyclecounter();
+#endif
 #pragma unroll
         for (int r0 = 0; r0 < NRT; r0 += RGN) {
           yfm_double4 acc[RGN];
@@ -459,15 +528,44 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
             for (int r = 0; r < RGN; ++r)
               acc[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(Af[r0 + r][kk], bvk[kk], acc[r], 0, 0, 0);
           // D[row = pair][col = step]: lane l holds step l & 15, pairs 16r + (l >> 4) + 4q
+#ifdef YFM_PROBE_NOWRITE  // timing probe: results kept in registers, never stored (the block reads stale z̃)
+#pragma unroll
+          for (int r = 0; r < RGN; ++r) asm volatile("" ::"a"(acc[r]));
+#else
 #pragma unroll
           for (int r = 0; r < RGN; ++r)
 #pragma unroll
             for (int q4 = 0; q4 < 4; ++q4)
               scr[(lane & 15) * SS + 16 * (r0 + r) + (lane >> 4) + 4 * q4] = acc[r][q4];
+#endif
         }
+#ifdef YFM_PROBE_MFMA2X  // timing probe: the block's MFMAs a second time, results discarded
+        double bvq[NK];  // opaque copies: the second pass must not be merged with the first
+#pragma unroll
+        for (int kk = 0; kk < NK; ++kk) {
+          bvq[kk] = bvk[kk];
+          asm volatile("" : "+v"(bvq[kk]));
+        }
+#pragma unroll
+        for (int r0 = 0; r0 < NRT; r0 += RGN) {
+          yfm_double4 acc[RGN];
+#pragma unroll
+          for (int r = 0; r < RGN; ++r) acc[r] = yfm_double4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int kk = 0; kk < NK; ++kk)
+#pragma unroll
+            for (int r = 0; r < RGN; ++r)
+              acc[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(Af[r0 + r][kk], bvq[kk], acc[r], 0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < RGN; ++r) asm volatile("" ::"a"(acc[r]));
+        }
+#endif
       }
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's scratch writes landed
       __builtin_amdgcn_wave_barrier();
+#ifdef YFM_PHASE_PROBE
+      const long long ph_b = __builtin_readcyclecounter();
+#endif
       const int tend = min(TB, nsteps - t0);
       // a block of steady steps: every lane of the wave frozen, and every step of the block a data
       // step of every lane (no NaN column, t ≥ 1, inside every lane's window)
@@ -478,10 +576,13 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
         if (__all(f.wave_frozen) && t0 >= 1 && t0 + tend <= wave_min_data) {
           // the block's NaN flags, one column per lane: one LDS round trip instead of tend serial ones
           // (0.236 → 0.217 ms at config 2, profiles/r3/probes/dns_steady_nan/)
-          const bool col_nan = (lane < tend) && (cb[min(lane, TB - 1) * LDP + NP + 2] != 0.0);
+          const bool col_nan = (lane < tend) && (col_flag != 0.0);
           blk_steady = !__any(col_nan);
         }
       }
+#ifdef YFM_PHASE_PROBE
+      const long long ph_c = __builtin_readcyclecounter();
+#endif
       // step operands for tt are read one step ahead (hides the LDS latency at 1 wave/SIMD)
       auto read_z = [&](int tt, double (&z)[NZ]) {  // this lane's pairs NZ·lane .. NZ·lane + NZ − 1
         const double* sp = scr + tt * SS + NZ * lane;
@@ -618,6 +719,20 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
       }
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();  // scratch reads done before the next block's writes
+#ifdef YFM_PHASE_PROBE
+      const long long ph_d = __builtin_readcyclecounter();
+      ph_bound += ph_a2 - ph_a;
+      ph_bload += ph_a3 - ph_a2;
+      ph_mfma += ph_b - ph_a3;
+      ph_dec += ph_c - ph_b;
+      if (blk_steady) {
+        ph_st += ph_d - ph_c;
+        ++ph_nst;
+      } else {
+        ph_full += ph_d - ph_c;
+        ++ph_nfull;
+      }
+#endif
       if constexpr (PIPE) {
         buf ^= 1;
         have_z = have_next;
@@ -656,6 +771,15 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     if (t < nsteps) half(t, zc, yb_c, meta_c, zn, yb_n, meta_n);
   }
 
+#ifdef YFM_PHASE_PROBE
+  if (lane == 0 && (blockIdx.x % 64) == 0)
+    printf("setup blk %d wave %d decode %lld loadings+G %lld frag %lld filter-setup %lld rest %lld\n", (int)blockIdx.x,
+           wave, ph_s1 - ph_entry, ph_s2 - ph_s1, ph_s3 - ph_s2, ph_s4 - ph_s3, ph_t0 - ph_s4);
+  if (lane == 0 && (blockIdx.x % 64) == 0)
+    printf("phase blk %d wave %d loop %lld setup %lld bound %lld bload %lld mfma+st %lld dec %lld steady %lld (%d) full %lld (%d)\n",
+           (int)blockIdx.x, wave, (long long)__builtin_readcyclecounter() - ph_t0, ph_t0 - ph_entry, ph_bound, ph_bload,
+           ph_mfma, ph_dec, ph_st, ph_nst, ph_full, ph_nfull);
+#endif
   if (!live || defer) return;
   const double ll = f.loglik(nobs, flags);
   out[b] = ll;
