@@ -8,6 +8,9 @@ set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-r4final}
 mkdir -p "$OUT"
+# the card's clocks, power and temperature before and after (box-to-box variation: one pass ran every config
+# 12-17% slower, TVλ included, whose kernel had not changed; profiles/r4/slow_box/)
+timeout -k 5 60 rocm-smi --showclocks --showpower --showtemp > "$OUT/smi_before.txt" 2>&1 || true
 ok() { local rc=$?; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "step exit $rc: stopping"; exit $rc; fi; }
 if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 700 python -u -m pytest tests -m gpu -v -s --timeout 240 --timeout-method thread --maxfail=20 \
@@ -43,3 +46,4 @@ done
 timeout -k 10 300 python -u tools/bench_estimate.py > "$OUT/bench_estimate.json" 2> "$OUT/bench_estimate.err"; ok
 timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/driver_cmd.json" 2> "$OUT/driver_cmd.err"; ok
 python3 -c "import json; d=json.load(open('$OUT/driver_cmd.json')); print('driver cmd', d['value'], d['ms_per_step'])"
+timeout -k 5 60 rocm-smi --showclocks --showpower --showtemp > "$OUT/smi_after.txt" 2>&1 || true
