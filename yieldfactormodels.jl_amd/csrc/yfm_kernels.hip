@@ -33,7 +33,7 @@
 namespace yfm {
 
 constexpr int kBlock = 256;  // 4 waves: one per SIMD of a CU
-constexpr int kTC = 32;      // panel columns per LDS chunk
+constexpr int kTC = 64;  // panel columns per LDS chunk (DNS; GNS5 and the pipelined DNS blocks keep 32 for LDS)
 constexpr bool kMfma4 = true;   // GNS5 Z'ỹ on v_mfma_f64_4x4x4_4b_f64 (DNS keeps v_mfma_f64_16x16x4_f64)
 constexpr bool kZBasis = true;  // GNS5 fragments e = 1 − e^{−λm} against (ỹ, ỹ/m): see the kernel
 #ifndef YFM_PIPE_VALU
@@ -144,12 +144,16 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     int rec_len, int* __restrict__ defer_list, int* __restrict__ defer_count, const double* __restrict__ init_rec,
     unsigned int* __restrict__ flags_next, int steady) {
   constexpr int LDP = NP + 4;
+  // panel columns per LDS chunk: 64 for DNS (a chunk rotation, with its two block barriers, every 64 steps
+  // instead of 32: 0.2040 → 0.2022 ms at config 2, profiles/r4/ab23/); 32 where the LDS is taken by GNS5's
+  // z̃ scratch or the pipelined block's second buffer
+  constexpr int TC = (M == 3 && !PIPE_) ? kTC : 32;
   constexpr bool USE_MFMA_ = (M - 1 == 2 || M - 1 == 4) && (NP <= 32);
   // frozen-covariance steady state (FixedZFilter): the loglik-mode DNS instantiation
   // with STEADY_ (the plain instantiation is the full recursion, YFM_DNS_STEADY=0)
   constexpr bool STEADY = STEADY_ && !RECORD && (M == 3 || M == 5) && USE_MFMA_;
   constexpr bool SPLIT_INIT = (M == 5);  // initial state from fixedz_init_kernel
-  constexpr int CH = kTC * LDP;               // doubles per chunk
+  constexpr int CH = TC * LDP;               // doubles per chunk
   constexpr int PER = (CH + kBlock - 1) / kBlock;
   constexpr int NZ = M - 1;                   // non-constant loading columns
   constexpr bool USE_MFMA = (NZ == 2 || NZ == 4) && (NP <= 32);  // fragments + LDS scratch budget
@@ -178,7 +182,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   constexpr int NBUF = PIPE ? 2 : 1;
   static_assert(NZ == 2 * LEAD, "loading columns come in (S, C) pairs per gamma");
   static_assert(NP % 2 == 0, "double2 panel reads");
-  static_assert(kTC % TB == 0, "MFMA blocks tile the panel chunk");
+  static_assert(TC % TB == 0, "MFMA blocks tile the panel chunk");
   __shared__ __attribute__((aligned(16))) double sh[2][CH];
   __shared__ __attribute__((aligned(16))) double scratch[kBlock / 64][NBUF][SCR];
   __shared__ int s_nobs_max;
@@ -395,7 +399,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     __syncthreads();
     load_chunk(2);
   }
-  auto col_of = [&](int t) -> const double* { return sh[(t / kTC) & 1] + (t % kTC) * LDP; };
+  auto col_of = [&](int t) -> const double* { return sh[(t / TC) & 1] + (t % TC) * LDP; };
 
   // one filter step given z̃_t (zc), (ȳ, ỹ'ỹ) and (nanflag, y'y) of column t
   auto do_step = [&](int t, const double (&zc)[NZ], double2 yb_c, double2 meta_c) {
@@ -407,9 +411,9 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
       if (live && !defer) f.record(t, b, my_steps, rec_len, rec_beta, rec_P);
     }
   };
-  auto rotate = [&](int t) {  // after step t: if chunk c = t / kTC is done, its buffer takes chunk c + 2
-    if ((t + 1) % kTC == 0) {
-      const int c = t / kTC;
+  auto rotate = [&](int t) {  // after step t: if chunk c = t / TC is done, its buffer takes chunk c + 2
+    if ((t + 1) % TC == 0) {
+      const int c = t / TC;
       __syncthreads();
       store_chunk(sh[c & 1]);
       __syncthreads();
