@@ -80,3 +80,15 @@ def test_create_model_mirror():
     np.testing.assert_array_equal(get_params(m), S.theta0_constrained(KIND_DNS))
     with pytest.raises(ValueError):
         set_params_(m, np.zeros(5))
+
+
+def test_build_keeps_agpr_spill_fence():
+    """DESIGN.md §5 / VERDICT r4 item 7: the library must be built with `-mllvm -amdgpu-spill-vgpr-to-agpr=0`
+    (ROCm 7.2 miscompiled the VGPR→AGPR spill path of the spilling GNS5 NP = 48 kernel;
+    tools/agpr_spill_repro/ reproduces it).  Dropping the fence from build_native.py fails here, loudly,
+    in the default CPU suite — and the stamp of the objects actually linked must carry it too."""
+    import build_native as BN
+    i = BN.FLAGS.index("-amdgpu-spill-vgpr-to-agpr=0")
+    assert BN.FLAGS[i - 1] == "-mllvm", BN.FLAGS
+    if BN.STAMP.exists():  # the library in the tree was linked from objects built with the fence
+        assert "-amdgpu-spill-vgpr-to-agpr=0" in BN.STAMP.read_text().split("\n")

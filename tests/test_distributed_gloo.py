@@ -41,6 +41,43 @@ def test_window_shards_cover_and_balance():
         assert max(per) - min(per) <= len(counts)
 
 
+def _steps_worker(rank, world, port, ret):
+    """bench.py's config-4 shard on this rank: Σ (T_use − 1) over its candidates, all-gathered as bench.py does."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    wins = np.arange(361, 601)
+    per = 4096
+    counts = [per] * len(wins)
+    idx = D.window_shards(counts, world, rank)
+    tu = np.repeat(wins, per)[idx]
+    mine = torch.tensor([float(np.sum(tu - 1)), float(len(idx))], dtype=torch.float64)
+    allr = torch.empty(2 * world, dtype=torch.float64)
+    dist.all_gather_into_tensor(allr, mine)
+    if rank == 0:
+        ret["steps"] = allr.view(world, 2)[:, 0].numpy().copy()
+        ret["n"] = allr.view(world, 2)[:, 1].numpy().copy()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_window_shards_equal_filter_steps(world):
+    """config 4's window shards give every rank the same Σ T_use (its filter steps, which
+    set its kernel time) to within one window's share — the longest window's steps once per window whose
+    4,096 candidates do not split evenly."""
+    mgr = mp.Manager()
+    ret = mgr.dict()
+    mp.spawn(_steps_worker, args=(world, _free_port(), ret), nprocs=world, join=True)
+    steps, n = ret["steps"], ret["n"]
+    assert n.sum() == 240 * 4096
+    if 4096 % world == 0:  # every window splits evenly: identical work per rank
+        assert steps.max() == steps.min()
+    # otherwise at most one window's per-rank share of filter steps apart
+    share = 4096 / world * 599
+    assert steps.max() - steps.min() <= share, (steps, share)
+    print(f"world {world}: per-rank filter steps {steps}, max/min {steps.max() / steps.min():.6f}")
+
+
 def _worker(rank, world, port, Theta, Y, mats, ret):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)

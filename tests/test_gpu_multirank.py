@@ -63,8 +63,11 @@ def test_bench_self_launches_n_ranks():
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1  # rank 0 only
     line = lines[0]
-    print({k: line[k] for k in ("n_gpus", "collective_world_size", "launcher", "value")})
+    print({k: line[k] for k in ("n_gpus", "collective_world_size", "launcher", "value", "per_rank_kernel_ms",
+                                "imbalance", "per_rank_filter_steps")})
     assert line["n_gpus"] == 2 and line["collective_world_size"] == 2
+    assert len(line["per_rank_kernel_ms"]) == 2 and min(line["per_rank_kernel_ms"]) > 0 and line["imbalance"] >= 1.0
+    assert line["per_rank_filter_steps"] == [4096 * 119] * 2
     assert line["config"]["global_batch"] == 2 * 4096 and "spawn_local_ranks" in line["launcher"]
 
 
@@ -84,6 +87,65 @@ def _rolling_worker(rank, world, port, Y, mats, out_dir, ret):
     ret[rank] = {wt: {k: v for k, v in res.items() if isinstance(v, np.ndarray)} for wt, res in out.items()}
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _driver_worker(rank, world, port, root, ret):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch  # noqa: F401
+    import torch.distributed as dist
+    sys.path[:0] = [str(ROOT), str(ROOT / "yieldfactormodels.jl_amd")]
+    import yfm_amd
+    os.chdir(root)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    model = yfm_amd.run("7", 44, 2, True, "1C", window_type="expanding", max_group_iters=1, iterations=20,
+                        seed=5, group=dist.group.WORLD)
+    info = model.last_run
+    ret[rank] = {"params": np.asarray(info["params"]), "files": list(info["files"]),
+                 "rolling": sorted(info.get("rolling", {}).keys())}
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _driver_inputs(root, Y, mats):
+    from yfm_amd import io as yio
+    d = root / "YieldFactorModels.jl" / "data"
+    d.mkdir(parents=True)
+    yio.writedlm(d / "thread_id__7__data.csv", Y)
+    yio.writedlm(d / "thread_id__7__maturities.csv", mats)
+
+
+def _tree(root):
+    return sorted(str(p.relative_to(root)) for p in root.rglob("*.csv"))
+
+
+def test_run_driver_two_ranks(engine, tmp_path):
+    """yfm_amd.run(group=…) with a MISSING init file on 2 ranks.  Rank 0 alone writes the random
+    start (broadcast to rank 1) and every result file; the CSV tree is exactly the single-process run's."""
+    from yfm_amd import io as yio
+    from yfm_amd import synthetic as S
+    import yfm_amd
+    mats = S.maturities_30()
+    Y = S.simulate_panel(0, 600)[:, :50].copy(order="F")
+    two, one = tmp_path / "two", tmp_path / "one"
+    for d in (two, one):
+        _driver_inputs(d, Y, mats)
+    mgr = mp.Manager()
+    ret = mgr.dict()
+    mp.spawn(_driver_worker, args=(2, _free_port(), str(two), ret), nprocs=2, join=True)
+    np.testing.assert_array_equal(ret[0]["params"], ret[1]["params"])  # the same start and estimate
+    assert ret[1]["files"] == [] and ret[1]["rolling"] == [] and ret[0]["files"]
+    cwd = os.getcwd()
+    os.chdir(one)
+    try:
+        model = yfm_amd.run("7", 44, 2, True, "1C", window_type="expanding", max_group_iters=1, iterations=20, seed=5)
+    finally:
+        os.chdir(cwd)
+    np.testing.assert_array_equal(model.last_run["params"], ret[0]["params"])
+    files = _tree(two)
+    assert files == _tree(one) and any("init_params_1C.csv" in f for f in files)
+    assert any("expanding_window_forecasts" in f for f in files)
+    for name in files:
+        np.testing.assert_array_equal(yio.readdlm(two / name), yio.readdlm(one / name), err_msg=name)
 
 
 def test_rolling_forecasts_two_ranks(engine, tmp_path):

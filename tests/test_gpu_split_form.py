@@ -21,6 +21,14 @@ from yfm_amd import synthetic as S
 
 pytestmark = pytest.mark.gpu
 
+# the regression is fenced by a build flag (build_native.py): refuse to run on a library built
+# without it, loudly (tools/agpr_spill_repro/ reproduces the miscompile on the last unfenced sources)
+import build_native as _BN  # noqa: E402
+
+if "-amdgpu-spill-vgpr-to-agpr=0" not in _BN.FLAGS or (_BN.STAMP.exists() and
+                                                       "-amdgpu-spill-vgpr-to-agpr=0" not in _BN.STAMP.read_text()):
+    raise RuntimeError("libyfm_hip.so must be built with -mllvm -amdgpu-spill-vgpr-to-agpr=0 (DESIGN.md §5)")
+
 
 def both_forms(engine, kind, Th, space=0, T_use=None):
     os.environ["YFM_DNS_STEADY"] = "0"  # the diagnostic instantiations are the full recursion

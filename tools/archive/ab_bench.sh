@@ -1,5 +1,5 @@
 # A/B of the in-tree library against yfm_amd/libyfm_hip_old.so on the given configs.
-# usage (via gpurun): bash tools/ab_bench.sh "2 5" [steps]
+# usage (via gpurun): bash tools/archive/ab_bench.sh "2 5" [steps]
 mkdir -p gpurun_out/ab
 CONFIGS=${1:-"2 5"}
 STEPS=${2:-100}

@@ -1,6 +1,6 @@
 #!/bin/bash
 # GNS5 (config 5) timing over several library builds + the GNS5 GPU tests on the first:
-# bash tools/ab_c5.sh <tag> <lib.so>...
+# bash tools/archive/ab_c5.sh <tag> <lib.so>...
 set -eo pipefail
 OUT=gpurun_out/$1; shift
 mkdir -p "$OUT"

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of two library builds: A = yfm_amd/libyfm_hip.so (in tree), B = tools/libyfm_hip_B.so.
-# usage: bash tools/ab_lib.sh <tag> [pytest -k expr]
+# usage: bash tools/archive/ab_lib.sh <tag> [pytest -k expr]
 set -eo pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-ab_lib}

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Timing A/B over several library builds: bash tools/ab_multi.sh <tag> <lib.so>... (each copied in place
+# Timing A/B over several library builds: bash tools/archive/ab_multi.sh <tag> <lib.so>... (each copied in place
 # of yfm_amd/libyfm_hip.so in turn; the in-tree build is restored at the end).  Optional PYTEST_K runs
 # the GPU tests matching it on the first library.
 set -eo pipefail

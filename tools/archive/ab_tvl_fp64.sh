@@ -1,5 +1,5 @@
 #!/bin/bash
-# FP64 TVλ (config 3) timing over several library builds: bash tools/ab_tvl_fp64.sh <tag> <lib.so>...
+# FP64 TVλ (config 3) timing over several library builds: bash tools/archive/ab_tvl_fp64.sh <tag> <lib.so>...
 set -eo pipefail
 OUT=gpurun_out/$1; shift
 mkdir -p "$OUT"

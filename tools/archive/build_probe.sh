@@ -2,7 +2,7 @@
 # Build a timing-probe variant of libyfm_hip.so (never the product library) into scratch/probe<N>/:
 #   YFM_TVL_PROBE=1  the TVλ kernels' 4×4 capacitance update replaced by a data-dependent no-op
 #   YFM_TVL_PROBE=2  the FP64 TVλ kernel counts, in the throw flag, the filters whose capacitance LU ever exchanges rows
-# usage: bash tools/build_probe.sh 1   → then YFM_LIB=scratch/probe1/libyfm_hip.so python bench.py ...
+# usage: bash tools/archive/build_probe.sh 1   → then YFM_LIB=scratch/probe1/libyfm_hip.so python bench.py ...
 set -eo pipefail
 N=${1:-1}
 OUT=scratch/probe$N

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build diagnostic variants of libyfm_hip.so into variants/ (git-ignored; they travel to the GPU box):
 # yfm_kernels.hip recompiled with extra flags, linked with the regular objects of build/.
-#   bash tools/dbg_variants.sh <name> "<extra hipcc flags>"
+#   bash tools/archive/dbg_variants.sh <name> "<extra hipcc flags>"
 set -eo pipefail
 cd "$(dirname "$0")/.."
 NAME=$1; EXTRA=$2

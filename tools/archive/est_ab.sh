@@ -1,4 +1,4 @@
-# Estimator timing under env variants (via gpurun): bash tools/est_ab.sh tag "ENV=.. ENV=.." ...
+# Estimator timing under env variants (via gpurun): bash tools/archive/est_ab.sh tag "ENV=.. ENV=.." ...
 TAG=${1:-est}; shift
 OUT=gpurun_out/$TAG
 mkdir -p $OUT

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build an experiment variant of libyfm_hip.so into variants/: the listed translation units recompiled with
 # extra flags, linked with the regular objects of build/ (git-ignored; travels to the GPU box).
-#   bash tools/exp_variant.sh <name> "<extra hipcc flags>" <tu> [<tu> ...]     (tu: yfm_kernels, yfm_capi, …)
+#   bash tools/archive/exp_variant.sh <name> "<extra hipcc flags>" <tu> [<tu> ...]     (tu: yfm_kernels, yfm_capi, …)
 set -eo pipefail
 cd "$(dirname "$0")/.."
 NAME=$1; EXTRA=$2; shift 2

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Submit one gpurun call, re-submitting ONLY while the pool has no free slot / box (status "transient":
 # nothing ran, nothing was charged).  A call that ran (pass or fail) is never repeated.
-# usage: bash tools/gpurun_retry.sh <timeout_s> <max_tries> '<command>'
+# usage: bash tools/archive/gpurun_retry.sh <timeout_s> <max_tries> '<command>'
 TO=$1; TRIES=$2; CMD=$3
 for i in $(seq 1 "$TRIES"); do
   out=$(/usr/local/graft/bin/gpurun --timeout "$TO" -- "$CMD" 2>&1)

@@ -2,7 +2,7 @@
 # Round-3 GPU pass: the -m gpu suite, the 3,000-seed randomised sweep (with the |ll|-denominator
 # report), then short config-2 / config-5 benches.  Each GPU step has its own time limit; the chain
 # stops at the first step that fails, times out or crashes.
-# usage (from the repo root, via gpurun): bash tools/r3_check.sh <tag> [pytest -k expr]
+# usage (from the repo root, via gpurun): bash tools/archive/r3_check.sh <tag> [pytest -k expr]
 set -eo pipefail
 export TMPDIR=/tmp
 TAG=${1:-r3}

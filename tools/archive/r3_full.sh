@@ -2,7 +2,7 @@
 # Full round-3 GPU pass: the -m gpu suite, then benches of configs 2-5 and the estimator, then a
 # rocprofv3 kernel-trace of the config-2 and config-3 benches.  Each GPU step has its own limit; the
 # chain stops at a crash/timeout (pytest assertion failures are reported and the benches still run).
-# usage: bash tools/r3_full.sh <tag>
+# usage: bash tools/archive/r3_full.sh <tag>
 set -eo pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-full}

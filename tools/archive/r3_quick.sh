@@ -1,6 +1,6 @@
 #!/bin/bash
 # Targeted GPU pass: selected -m gpu tests, then one default bench line (with the CPU baseline).
-# usage: bash tools/r3_quick.sh <tag> "<pytest -k expr>" [bench args...]
+# usage: bash tools/archive/r3_quick.sh <tag> "<pytest -k expr>" [bench args...]
 set -eo pipefail
 export TMPDIR=/tmp
 TAG=$1; K=$2; shift 2

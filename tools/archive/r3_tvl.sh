@@ -1,7 +1,7 @@
 #!/bin/bash
 # TVλ GPU pass: the TVλ / edge / states GPU tests, then config-3 benches (certified, FP64) and
 # optionally the selective-certification probe.  Each GPU step has its own time limit; the chain
-# stops at the first failure.   usage: bash tools/r3_tvl.sh <tag> [probe]
+# stops at the first failure.   usage: bash tools/archive/r3_tvl.sh <tag> [probe]
 set -eo pipefail
 export TMPDIR=/tmp
 TAG=${1:-tvl}

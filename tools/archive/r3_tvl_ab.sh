@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of certified-TVλ library builds: accuracy on the 1,024-candidate config-3 fixture and config-3
-# throughput, per library.   usage: bash tools/r3_tvl_ab.sh <tag> lib1.so lib2.so ...
+# throughput, per library.   usage: bash tools/archive/r3_tvl_ab.sh <tag> lib1.so lib2.so ...
 set -eo pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-tvl_ab}

@@ -2,7 +2,7 @@
 # Generic A/B of variants/libyfm_<v>.so builds (VARS, the first is the reference): bitwise check of the DNS
 # logliks against the first, config 2 alternated (REPS), config 5 once each (C5=1), phase probes (PROBES), and
 # the DNS/GNS5 GPU tests on TESTLIB.
-#   VARS="cur unr" PROBES="phcur phunr" TESTLIB=unr bash tools/r4_ab.sh <outdir under gpurun_out/>
+#   VARS="cur unr" PROBES="phcur phunr" TESTLIB=unr bash tools/archive/r4_ab.sh <outdir under gpurun_out/>
 set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-r4ab}

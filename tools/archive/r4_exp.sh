@@ -1,6 +1,6 @@
 #!/bin/bash
-# Same-box timing A/B of config 2 over variant libraries (tools/exp_variant.sh), alternated twice.
-#   bash tools/r4_exp.sh <tag> <lib-name> [<lib-name> ...]     (lib-name: a variants/libyfm_<name>.so, or "new")
+# Same-box timing A/B of config 2 over variant libraries (tools/archive/exp_variant.sh), alternated twice.
+#   bash tools/archive/r4_exp.sh <tag> <lib-name> [<lib-name> ...]     (lib-name: a variants/libyfm_<name>.so, or "new")
 set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/$1; shift

@@ -3,7 +3,7 @@
 # config 2-5 the PMC passes (one counter group per run, each under a hard limit) with their per-kernel
 # summary, the rocprofv3 kernel statistics, and the bench line (which reads the PMC summary for
 # roofline.traffic), then the rolling re-estimation benchmark and the driver's own bench command.
-#   bash tools/r4_final.sh <outdir under gpurun_out/>      (SKIP_TESTS=1: no pytest/smoke)
+#   bash tools/archive/r4_final.sh <outdir under gpurun_out/>      (SKIP_TESTS=1: no pytest/smoke)
 set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-r4final}

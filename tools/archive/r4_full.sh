@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 GPU pass: the whole -m gpu suite, the default bench line, smoke.  Stops at a fault / abort /
 # timeout (pytest exit status other than 0 or 1).
-# usage: bash tools/r4_full.sh <tag>
+# usage: bash tools/archive/r4_full.sh <tag>
 set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-r4full}

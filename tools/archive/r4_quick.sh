@@ -2,7 +2,7 @@
 # Targeted GPU pass: selected -m gpu tests (pytest -k), then one bench line.
 # Stops at a fault / abort / timeout (exit status other than 0 or 1 from pytest); plain test failures
 # (status 1) still run the bench.
-# usage: bash tools/r4_quick.sh <tag> "<pytest -k expr>" [bench args...]     (NOBENCH=1: skip the bench)
+# usage: bash tools/archive/r4_quick.sh <tag> "<pytest -k expr>" [bench args...]     (NOBENCH=1: skip the bench)
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1; K=$2; shift 2

@@ -1,6 +1,6 @@
 """Accuracy of the certified TVλ filter of the library YFM_LIB points at (default: the in-tree build) on the
 1,024-candidate config-3 fixture (tests/golden/config3/tvl_config3_1024.npz): error distribution against the
-binary128 truth, and the factor-1 parity table.  One JSON line.  (A/B helper: tools/r3_tvl_ab.sh.)"""
+binary128 truth, and the factor-1 parity table.  One JSON line.  (A/B helper: tools/archive/r3_tvl_ab.sh.)"""
 from __future__ import annotations
 
 import json

@@ -37,8 +37,21 @@ def _deps():
     return list(CSRC.glob("*")) + list((ROOT / "include").glob("*.h")) + [Path(__file__)]
 
 
+STAMP = BUILD / "flags.stamp"
+
+
+def _stamp() -> str:
+    """The compiler, target and flags the objects in build/ were made with: a different stamp forces a full
+    rebuild (objects for another arch or flag set must never be linked together)."""
+    return "\n".join([HIPCC, ARCH, *FLAGS]) + "\n"
+
+
+def _stamp_ok() -> bool:
+    return STAMP.exists() and STAMP.read_text() == _stamp()
+
+
 def up_to_date() -> bool:
-    if not LIB.exists():
+    if not LIB.exists() or not _stamp_ok():
         return False
     t = LIB.stat().st_mtime
     return all(p.stat().st_mtime <= t for p in _deps())
@@ -48,6 +61,8 @@ def build(force: bool = False, verbose: bool = True) -> Path:
     if not force and up_to_date():
         return LIB
     BUILD.mkdir(exist_ok=True)
+    if not _stamp_ok():
+        force = True
     srcs = _sources()
     objs = [BUILD / (s.stem + ".o") for s in srcs]
 
@@ -64,8 +79,11 @@ def build(force: bool = False, verbose: bool = True) -> Path:
               + [Path(__file__).stat().st_mtime])
     todo = [(s, o) for s, o in zip(srcs, objs)
             if force or not o.exists() or o.stat().st_mtime < max(s.stat().st_mtime, hdr)]
+    if todo:
+        STAMP.unlink(missing_ok=True)  # a half-finished rebuild must not pass as the stamped one
     with ThreadPoolExecutor(max_workers=max(1, min(len(todo), 4))) as ex:
         list(ex.map(cc, todo))
+    STAMP.write_text(_stamp())
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(LIB)]
     if verbose:
         print(" ".join(cmd), flush=True)

@@ -236,7 +236,9 @@ __global__ __launch_bounds__(kFdBlock) void fixedz_dd_loglik_kernel(
   for (int base = blockIdx.x * GPB; base < nd; base += gridDim.x * GPB) {  // block-uniform bound
   const int g = base + grp;
   const bool live = g < nd;
-  const int gg = live ? g : 0;
+  // an idle group reads the record of this block's first group (base < nd: written above by this same
+  // workgroup before the barrier), never one another block may still be writing
+  const int gg = live ? g : base;
   const int b = defer_list[gg];
   const int nobs = T_use ? T_use[b] : T;
 

@@ -21,6 +21,7 @@ import os
 import socket
 import subprocess
 import sys
+import time
 from dataclasses import dataclass
 from typing import Callable
 
@@ -53,12 +54,13 @@ def spawn_local_ranks(script: str, argv: list[str], nprocs: int, env: dict | Non
         e = dict(base, RANK=str(r), LOCAL_RANK=str(r))
         procs.append(subprocess.Popen([sys.executable, script, *argv], env=e))
     rc = 0
+    deadline = None if timeout is None else time.monotonic() + timeout
     try:
         pending = list(procs)
         while pending:
             for p in list(pending):
                 try:
-                    code = p.wait(timeout=0.2)
+                    code = p.wait(timeout=0.2 / len(pending))
                 except subprocess.TimeoutExpired:
                     continue
                 pending.remove(p)
@@ -66,12 +68,10 @@ def spawn_local_ranks(script: str, argv: list[str], nprocs: int, env: dict | Non
                     rc = code
                     for q in pending:
                         q.terminate()
-            if timeout is not None:
-                timeout -= 0.2
-                if timeout <= 0:
-                    for q in pending:
-                        q.kill()
-                    return rc or 124
+            if deadline is not None and pending and time.monotonic() >= deadline:
+                for q in pending:
+                    q.kill()
+                return rc or 124
     finally:
         for p in procs:
             if p.poll() is None:

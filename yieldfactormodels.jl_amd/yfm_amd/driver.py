@@ -134,6 +134,19 @@ def run_estimation_(model: AbstractKalmanModel, data, in_sample_end: int, all_pa
     return init_p, ll, best_p, ir
 
 
+def _rank(group) -> int:
+    import torch.distributed as dist
+    return dist.get_rank(group)
+
+
+def _broadcast_from_lead(arr, group) -> np.ndarray:
+    """Rank 0's array on every rank of `group` (a pickled object broadcast; a few hundred bytes)."""
+    import torch.distributed as dist
+    box = [arr]
+    dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+    return np.array(box[0], dtype=np.float64)
+
+
 def run(thread_id: str = "1", in_sample_end: int = 100, forecast_horizon: int = 12, run_rolling: bool = True,
         model_type: str = "1C", float_type=np.float64, *, window_type: str = "both", in_sample_start: int = 1,
         param_groups=(), max_group_iters: int = 10, group_tol: float = 1e-8, run_optimization: bool = True,
@@ -158,9 +171,19 @@ def run(thread_id: str = "1", in_sample_end: int = 100, forecast_horizon: int = 
     model, model_type = create_model(model_type, maturities, N, M, float_type,
                                      results_location=f"{results_location}{model_type}/")
     param_groups = get_param_groups(model, param_groups)
-    all_params = np.array(load_initial_parameters_(model, model_type, float_type, simulation, rng), dtype=np.float64)
-    if all_params.ndim == 1:
-        all_params = all_params[:, None]
+    # With a group, rank 0 alone reads (or writes) the init file and every file below; the start is then
+    # broadcast, so no rank reads a file another one is still writing (the estimation before the rolling
+    # forecasts is deterministic: every rank computes the same parameters, only rank 0 saves them).
+    lead = group is None or _rank(group) == 0
+    all_params = None
+    if lead:
+        all_params = np.array(load_initial_parameters_(model, model_type, float_type, simulation, rng),
+                              dtype=np.float64)
+        if all_params.ndim == 1:
+            all_params = all_params[:, None]
+    if group is not None:
+        all_params = _broadcast_from_lead(all_params, group)
+    save_results_bool = save_results_bool and lead
     set_params_(model, all_params[:, 0])
     all_params[:, 0] = load_static_parameters_(model, model_type, results_location, thread_id, all_params[:, 0])
     info = {"files": []}
