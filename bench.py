@@ -595,16 +595,29 @@ def main():
         finally:
             os.environ.pop("YFM_DNS_STEADY", None)
         fin = np.isfinite(full_host)
-        dr = np.abs(out_host[fin] - full_host[fin]) / np.abs(full_host[fin])
+        da = np.abs(out_host[fin] - full_host[fin])
+        dr = da / np.abs(full_host[fin])
+        worst = None
+        if dr.size:
+            k = int(np.argmax(dr))
+            gi = int(np.flatnonzero(fin)[k])
+            worst = {"index": gi, "loglik": float(full_host[gi]), "rel": float(dr[k]), "abs": float(da[k]),
+                     "window": int(Tb[gi])}
         steady = {"steady_lane_steps": 64 * steady_ws, "frac_of_filter_steps": 64 * steady_ws / float(np.sum(Tb - 1)),
                   "full_recursion_evals_per_s": w.global_batch / (wall_full / args.steps),
                   "full_recursion_kernel_ms": kms_full,
                   "vs_full_recursion_max_rel": float(dr.max()) if dr.size else 0.0,
+                  "vs_full_recursion_max_abs": float(da.max()) if da.size else 0.0,
+                  "vs_full_recursion_worst": worst,
+                  "vs_full_recursion_max_rel_abs_ll_ge_1": float(dr[np.abs(full_host[fin]) >= 1.0].max())
+                  if np.any(np.abs(full_host[fin]) >= 1.0) else 0.0,
                   "pattern_match": bool(np.array_equal(np.isfinite(out_host), fin)),
                   "note": "the covariance recursion of filter.jl:158-176 is data-independent for fixed loadings; each "
                           "candidate freezes P once its change per step is at the rounding level (a step set by its "
                           "own θ), a wave whose candidates are all frozen runs the mean update only "
-                          "(DESIGN.md §3.1; YFM_DNS_STEADY=0 disables it)"}
+                          "(DESIGN.md §3.1; YFM_DNS_STEADY=0 disables it).  The relative change is against |loglik|: "
+                          "a loglik near 0 (a sum of ~10^4-sized terms that cancels) shows a large relative change "
+                          "for a rounding-sized absolute one — see vs_full_recursion_worst and the |ll| ≥ 1 column"}
     n_neginf, n_nan = int(np.isneginf(out_host).sum()), int(np.isnan(out_host).sum())
     n_deferred = eng.last_deferred()  # candidates of the last timed batch on the double-double path
 

@@ -18,8 +18,8 @@ from yfm_amd import params as PR  # noqa: E402
 
 eng = get_engine(0)
 for case in [int(a) for a in sys.argv[1:]] or [9]:
-    kind, T, reg = CASES[case]
-    N, mats, Y, Th, space, T_use, pattern = make_case(kind, T, reg, 7000 + case)
+    kind, T, reg, pattern, space = CASES[case]
+    N, mats, Y, Th, T_use = make_case(kind, T, reg, pattern, space, 7000 + case)
     eng.set_panel(Y, mats)
     os.environ["YFM_GNS5_STEADY"] = "1"
     got = eng.loglik(kind, Th, space=space, T_use=T_use)

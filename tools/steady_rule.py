@@ -11,6 +11,10 @@ Rules:
   contract  round 4: d = 0, or d ≤ 2^-46 and M·d·C ≤ 2^-50 with C = Σ_{k≥1} ‖A^k‖_F² bounded from
             A = Φ R S⁻¹ (the closed-loop matrix; exact Riccati difference identity
             P_{t+2} − P_{t+1} = A_{t+1} (P_{t+1} − P_t) A_t')
+  gain      round 5 (the kernel's rule): contract at 2^-52, and the loglik's sensitivity
+            max(1, C₁)·‖P‖_∞‖S⁻¹‖_∞ ≤ 512 with C₁ = Σ_{k≥1} ‖A^k‖_∞ (else only d = 0 freezes) — a frozen P's
+            rounding-level error moves c'S⁻¹c by ‖ΔP‖‖S⁻¹‖ and the filtered mean by C₁‖ΔK‖
+            (yfm_fixedz.hpp contraction_bound)
 
     python tools/steady_rule.py [--B 4096] [--T 600]
 """
@@ -62,16 +66,23 @@ def loadings(g, mats):
     return np.stack(cols, 2)  # B, N, M
 
 
-def contraction_C(Phi, R, Sm, M):
+def contraction_C(Phi, R, Sm, M, P=None, cap=None):
     """Upper bound of Σ_{k≥1} ‖A^k‖_∞² for A = Φ R S⁻¹ (inf where ‖A⁴‖_∞ ≥ 1), as the device's
-    contraction_bound (yfm_fixedz.hpp) with its 1.01 rounding margin."""
+    contraction_bound (yfm_fixedz.hpp) with its 1.01 rounding margin; with `cap`, also inf where the
+    loglik sensitivity max(1, C₁)‖P‖_∞‖S⁻¹‖_∞ exceeds it (C₁ = Σ_{k≥1} ‖A^k‖_∞)."""
     A = Phi @ np.swapaxes(np.linalg.solve(Sm, R), 1, 2)  # R S⁻¹ = (S⁻¹R)'
     A2 = A @ A
     A3 = A2 @ A
     A4 = A2 @ A2
-    n = [np.max(np.sum(np.abs(X), axis=2), axis=1) ** 2 for X in (A, A2, A3, A4)]
+    r = [np.max(np.sum(np.abs(X), axis=2), axis=1) for X in (A, A2, A3, A4)]
+    n = [x ** 2 for x in r]
     with np.errstate(divide="ignore", invalid="ignore"):
         C = np.where(n[3] < 1.0, 1.01 * (n[0] + n[1] + n[2] + n[3]) / (1.0 - n[3]), np.inf)
+        if cap is not None:
+            c1 = 1.01 * (r[0] + r[1] + r[2] + r[3]) / (1.0 - r[3])
+            inf_norm = lambda X: np.max(np.sum(np.abs(X), axis=2), axis=1)  # noqa: E731
+            gain = np.maximum(1.0, c1) * inf_norm(P) * inf_norm(np.linalg.inv(Sm))
+            C = np.where(gain <= cap, C, np.inf)
     return C
 
 
@@ -132,7 +143,8 @@ def run(kind, Y, mats, Thc, rule=None, tau=2.0 ** -50):
                 ok = (d <= 2.0 ** -46) & (rho < 0.999) & (d * rho <= tau * (1 - rho))
             db = np.where(ok, d * rho / np.maximum(1 - rho, 1e-300), 0)
         else:
-            C = 2.0 * contraction_C(Phi, R, P + R, M)  # the device's 2C (first-order margin)
+            cap = 512.0 if rule == "gain" else None
+            C = 2.0 * contraction_C(Phi, R, P + R, M, P, cap)  # the device's 2C (first-order margin)
             ok = (d == 0) | ((d <= 2.0 ** -46) & (d * C <= tau))
             db = np.where(d == 0, 0.0, d * C)
         newf = ok & ~frozen
@@ -186,8 +198,8 @@ def main():
     ap.add_argument("--B", type=int, default=2048)
     ap.add_argument("--T", type=int, default=600)
     ap.add_argument("--kind", type=int, default=KIND_DNS)
-    ap.add_argument("--rules", default="r3,contract")
-    ap.add_argument("--taus", default="50", help="comma list of k: freeze when d·2C ≤ 2^-k (contract rule)")
+    ap.add_argument("--rules", default="contract,gain")
+    ap.add_argument("--taus", default="52", help="comma list of k: freeze when d·2C ≤ 2^-k (contract, gain rules)")
     a = ap.parse_args()
     kind = a.kind
     mats = S.maturities_30()
@@ -197,9 +209,9 @@ def main():
         full, *_ = run(kind, Y, mats, Thc)
         fin = np.isfinite(full)
         print(f"== {name}: {fin.sum()} finite of {a.B}")
-        for rule, k in [(r, k) for r in a.rules.split(",") for k in (a.taus.split(",") if r == "contract" else ["50"])]:
+        for rule, k in [(r, k) for r in a.rules.split(",") for k in (a.taus.split(",") if r in ("contract", "gain") else ["50"])]:
             ll, fs, db, sens = run(kind, Y, mats, Thc, rule, 2.0 ** -int(k))
-            rule = f"{rule}{k}" if rule == "contract" else rule
+            rule = f"{rule}{k}" if rule in ("contract", "gain") else rule
             e = np.abs(ll[fin] - full[fin])
             rel = e / np.abs(full[fin])
             w = fs[: (a.B // 64) * 64].reshape(-1, 64).max(1)

@@ -205,8 +205,20 @@ __device__ __forceinline__ void propagate_cov_freeze(const Params<M, LEAD>& p, c
 // that moved P by δ is ‖Σ_{k≥1} δ_{t+k}‖_max ≤ C ‖δ‖_max — whatever the eigenvalues of A (real or
 // complex, monotone or oscillating convergence).  From A … A⁴ by sub-multiplicativity:
 // C ≤ (‖A‖² + ‖A²‖² + ‖A³‖² + ‖A⁴‖²)/(1 − ‖A⁴‖²); +Inf when ‖A⁴‖_∞ ≥ 1 (no bound: never frozen early).
+//
+// The loglik's sensitivity (round 5; the de-aliased sweep's case 9: a 1.3e-11 loglik change).  Within 2^-52 of
+// the full recursion's P is not enough by itself: a frozen P that differs from it by ΔP changes each innovation
+// term c'S⁻¹c by c'S⁻¹ΔP S⁻¹c, i.e. relatively by up to ‖ΔP‖‖S⁻¹‖ ≈ 2^-52·‖P‖‖S⁻¹‖, and the filtered mean
+// carries the gain change ΔK = R S⁻¹ΔP S⁻¹ through the closed loop, ‖Δβ_t‖ ≤ C₁‖ΔK‖ max‖c‖ with
+// C₁ = Σ_{k≥1} ‖A^k‖_∞ ≤ (‖A‖ + ‖A²‖ + ‖A³‖ + ‖A⁴‖)/(1 − ‖A⁴‖).  A lane is allowed to freeze short of a bitwise
+// fixed point only when g = max(1, C₁)·‖P‖_∞‖S⁻¹‖_∞ ≤ kLoglikGainCap (else C = +Inf: d = 0 only), which keeps
+// the relative loglik change near 512·2^-52 ≈ 1e-13 unless the loglik itself cancels.  Calibrated with the CPU
+// model of the rule (tools/steady_rule.py --rules gain): the case-9 class 6.8e-12 → 1.8e-14; the config-2
+// class (g ≤ 22) keeps every freeze; θ₀ ± 0.3 has 0.1% of its lanes above the cap.
 // Row j of A^k is (A')^k e_j, A'v = S⁻¹(R(Φ'v)): no M×M temporaries beyond the factors of S (the
 // GNS5 kernel has no registers for A and its powers; M ≤ 3 runs the M start vectors side by side).
+constexpr double kLoglikGainCap = 512.0;
+
 template <int M, int LEAD>
 __device__ __forceinline__ double contraction_bound(const Params<M, LEAD>& p, const double (&R)[M][M],
                                                     const double (&Pm)[M][M]) {
@@ -218,6 +230,7 @@ __device__ __forceinline__ double contraction_bound(const Params<M, LEAD>& p, co
   LDLT<M> f;
   (void)f.factor(S);
   double n[4] = {0.0, 0.0, 0.0, 0.0};  // ‖A^k‖_∞, k = 1..4
+  double sinv = 0.0;                   // ‖S⁻¹‖_∞ (S⁻¹ symmetric: the largest column sum of |S⁻¹ e_j|)
   // one row of A^k per start vector e_j: v ← S⁻¹R Φ'v, ‖A^k‖_∞ = max_j Σ_i |v_i|
   auto power_step = [&](double (&v)[M]) {
     double w[M];
@@ -241,6 +254,16 @@ __device__ __forceinline__ double contraction_bound(const Params<M, LEAD>& p, co
     for (int i = 0; i < M; ++i) sum += fabs(v[i]);
     return sum;
   };
+  auto sinv_col = [&](int j) {  // Σ_i |(S⁻¹ e_j)_i|
+    double v[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) v[i] = (i == j) ? 1.0 : 0.0;
+    f.solve(v);
+    double sum = 0.0;
+#pragma unroll
+    for (int i = 0; i < M; ++i) sum += fabs(v[i]);
+    return sum;
+  };
   if constexpr (M <= 3) {
     // the M start vectors side by side: M independent chains per power (the rolled form below is one
     // serial chain of 4M solves, ≈ 3 µs of a config-2 launch; profiles/r4/exp1/)
@@ -250,6 +273,8 @@ __device__ __forceinline__ double contraction_bound(const Params<M, LEAD>& p, co
 #pragma unroll
       for (int i = 0; i < M; ++i) V[j][i] = (i == j) ? 1.0 : 0.0;
 #pragma unroll
+    for (int j = 0; j < M; ++j) sinv = fmax(sinv, sinv_col(j));
+#pragma unroll
     for (int k = 0; k < 4; ++k)
 #pragma unroll
       for (int j = 0; j < M; ++j) n[k] = fmax(n[k], power_step(V[j]));
@@ -257,6 +282,7 @@ __device__ __forceinline__ double contraction_bound(const Params<M, LEAD>& p, co
     // (GNS5: one column and one power at a time keeps the temporaries to two M-vectors)
 #pragma unroll 1
     for (int j = 0; j < M; ++j) {
+      sinv = fmax(sinv, sinv_col(j));
       double v[M];
 #pragma unroll
       for (int i = 0; i < M; ++i) v[i] = (i == j) ? 1.0 : 0.0;
@@ -270,10 +296,20 @@ __device__ __forceinline__ double contraction_bound(const Params<M, LEAD>& p, co
       }
     }
   }
+  double pn = 0.0;  // ‖P‖_∞
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < M; ++j) s += fabs(Pm[i][j]);
+    pn = fmax(pn, s);
+  }
   const double n0 = n[0], n1 = n[1], n2 = n[2], n3 = n[3];
   const double q = n3 * n3;
-  // rounding of the bound itself: a few ulps; the 1.01 margin covers it
-  return (q < 1.0) ? 1.01 * (n0 * n0 + n1 * n1 + n2 * n2 + q) / (1.0 - q) : __builtin_inf();
+  // rounding of the bounds themselves: a few ulps; the 1.01 margins cover it
+  const double c1 = 1.01 * (n0 + n1 + n2 + n3) / (1.0 - n3);
+  const bool ok = (q < 1.0) && (fmax(1.0, c1) * pn * sinv <= kLoglikGainCap);
+  return ok ? 1.01 * (n0 * n0 + n1 * n1 + n2 * n2 + q) / (1.0 - q) : __builtin_inf();
 }
 
 template <int M, int LEAD, bool RECORD, bool STEADY = false, bool SPLIT_FORM = false>
@@ -299,7 +335,8 @@ struct FixedZFilter {
   //   A = Φ R S⁻¹ (contraction_bound, computed once, prepare_bound), so every later P of the
   //   full recursion is within 2^-52 (relative to its largest entry, to first order in d) of the frozen
   //   one — inside the FP64 recursion's own rounding jitter — for monotone and oscillating
-  //   (complex-eigenvalue) convergence alike (DESIGN.md §3.1 carries the bound on the loglik);
+  //   (complex-eigenvalue) convergence alike (DESIGN.md §3.1 carries the bound on the loglik); and the
+  //   loglik's sensitivity max(1, C₁)‖P‖‖S⁻¹‖ ≤ 512 (contraction_bound: else only d = 0 freezes);
   // a frozen lane keeps P (and so S = P + R and its factors) for every later data step, until a
   // prediction-only step (a NaN column) moves P.  The freeze step depends on the lane's θ alone, so its
   // loglik does not depend on the batch.  Once EVERY lane of a wave is frozen the wave runs the mean
