@@ -51,9 +51,12 @@ from yfm_amd import distributed as D  # noqa: E402
 from yfm_amd import synthetic as S  # noqa: E402
 
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector, AMD spec (the local guide lists no FP64 figure)
-# v_fma_f64 microbenchmark at steady clock (tools/fp64_peak.hip, profiles/r1/fp64_peak.txt):
-# 42.9 TFLOP/s at 1 wave per SIMD, 44.7 at 2, 68.7 at 8
-FP64_MEASURED_TFLOPS = 68.7
+# v_fma_f64 microbenchmark at steady clock, straight-line (tools/fp64_waves.hip, profiles/r5/micro/fp64_waves.txt):
+# 76.1 TFLOP/s at 8 waves per SIMD, 72.7 at ONE wave per SIMD with 32 independent chains (62.2 with 4).  (The
+# round-1 probe, tools/fp64_peak.hip, kept its loop branch in every 16 FMAs and read 42.9 at one wave: loop overhead,
+# not a one-wave issue limit.)
+FP64_MEASURED_TFLOPS = 76.1
+FP64_ONE_WAVE_TFLOPS = 72.7
 METRIC = "Kalman loglik evals/sec (DNS, T=600, N=30)"
 
 
@@ -384,7 +387,8 @@ def roofline(kind, prec, N, M, T, T_use, B, P, kernel_ms, steady_lane_steps=0):
     exe_tf = exe * steps / (kernel_ms * 1e-3) / 1e12 if exe else None
     return {"bound": "fp64-valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": achieved / FP64_PEAK_TFLOPS, "frac_vs_measured_peak": achieved / FP64_MEASURED_TFLOPS,
-            "measured_peak": FP64_MEASURED_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
+            "measured_peak": FP64_MEASURED_TFLOPS, "one_wave_peak": FP64_ONE_WAVE_TFLOPS,
+            "traffic": traffic, "traffic_source": traffic_src,
             "algorithmic_bytes": B * (P + 1) * 8 + T * (N + 4) * 8, "kernel": name, "kernel_ms": kernel_ms,
             "flops_per_eval": f_rank / max(B, 1),
             "flop_model": ("SURVEY §8d capacitance form (62N + 939 per step)" if kind == KIND_TVL else
@@ -396,7 +400,8 @@ def roofline(kind, prec, N, M, T, T_use, B, P, kernel_ms, steady_lane_steps=0):
             "executed_frac_vs_measured_peak": exe_tf / FP64_MEASURED_TFLOPS if exe_tf else None,
             "note": "kernel_ms = HIP events around each library call in the timed region, on its stream "
                     "(TVλ: init + filter kernels); executed_* = PMC-counted FP64 flops of the same kernel "
-                    "(profiles/); peak = AMD spec, measured_peak = v_fma_f64 microbenchmark at 8 waves/SIMD"
+                    "(profiles/); peak = AMD spec, measured_peak = v_fma_f64 microbenchmark at 8 waves/SIMD "
+                    "(one_wave_peak: at one wave/SIMD, the occupancy of these kernels)"
                     + ("; certified precision runs the same algorithm in double-double (≈7× the FP64 "
                        "instructions), frac is of the algorithm's FP64 count" if kind == KIND_TVL and prec == "certified"
                        else "")}
