@@ -50,8 +50,23 @@ __global__ __launch_bounds__(256, 1) void probe(const double* __restrict__ init,
   }
   __syncthreads();
   double sumq = 0.0;
+  long long csteady = 0;
   const long long c0 = __builtin_readcyclecounter();
   for (int blk = 0; blk < NB; ++blk) {
+    // a new block of operands per block (the kernel's MFMA block writes them): not loop-invariant
+    {
+      const double pert = 1e-9 * blk;
+#pragma unroll
+      for (int t = 0; t < TB; ++t) {
+        double2* q = reinterpret_cast<double2*>(&zs[wave][t][lane][0]);
+        double2 v = q[0];
+        v.x += pert;
+        q[0] = v;
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+    }
+    const long long cs = __builtin_readcyclecounter();
 #pragma unroll
     for (int t = 0; t < TB; ++t) {
       const double2 z = *reinterpret_cast<const double2*>(&zs[wave][t][lane][0]);
@@ -110,10 +125,19 @@ __global__ __launch_bounds__(256, 1) void probe(const double* __restrict__ init,
         for (int i = 0; i < M; ++i) beta[i] = nb[i];
       }
     }
+#pragma unroll
+    for (int i = 0; i < M; ++i) asm volatile("" ::"v"(beta[i]));
+    asm volatile("" ::"v"(sumq));
+    csteady += __builtin_readcyclecounter() - cs;
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
   }
   const long long c1 = __builtin_readcyclecounter();
   out[b] = sumq + beta[0] + beta[1] + beta[2];
-  if (lane == 0) cyc[b >> 6] = c1 - c0;
+  if (lane == 0) {
+    cyc[2 * (b >> 6)] = c1 - c0;
+    cyc[2 * (b >> 6) + 1] = csteady;
+  }
 }
 
 template <int V>
@@ -133,18 +157,18 @@ static void run(const double* d_init, double* d_out, long long* d_cyc, int B) {
     hipEventElapsedTime(&ms, e0, e1);
     best = ms < best ? ms : best;
   }
-  long long* h = new long long[waves];
-  hipMemcpy(h, d_cyc, sizeof(long long) * waves, hipMemcpyDeviceToHost);
-  double mean = 0;
-  long long mx = 0;
+  long long* h = new long long[2 * waves];
+  hipMemcpy(h, d_cyc, sizeof(long long) * 2 * waves, hipMemcpyDeviceToHost);
+  double mean = 0, mst = 0;
   for (int w = 0; w < waves; ++w) {
-    mean += h[w];
-    mx = h[w] > mx ? h[w] : mx;
+    mean += h[2 * w];
+    mst += h[2 * w + 1];
   }
   mean /= waves;
-  printf("V=%d (%s): %.4f ms, cycles per steady step: mean %.1f, max %.1f (per-wave s_memtime over %d steps)\n", V,
+  mst /= waves;
+  printf("V=%d (%s): %.4f ms; s_memtime ticks per step: whole loop %.1f, steady steps only %.1f (%d steps)\n", V,
          V == 0 ? "kernel form, chain ~12 deep" : "time-invariant form, chain 3 deep", best, mean / (NB * TB),
-         (double)mx / (NB * TB), NB * TB);
+         mst / (NB * TB), NB * TB);
   delete[] h;
 }
 
@@ -154,7 +178,7 @@ int main() {
   long long* d_cyc;
   hipMalloc(&d_init, 1024 * 8);
   hipMalloc(&d_out, B * 8);
-  hipMalloc(&d_cyc, (B / 64) * 8);
+  hipMalloc(&d_cyc, (B / 64) * 16);
   double h[1024];
   for (int i = 0; i < 1024; ++i) h[i] = 0.5 + 0.001 * ((i * 7919) % 997);
   hipMemcpy(d_init, h, sizeof h, hipMemcpyHostToDevice);
