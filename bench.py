@@ -588,6 +588,8 @@ def main():
     steady_ws = eng.last_steady() if kind in (KIND_DNS, KIND_GNS) else 0  # frozen-covariance wave-steps of the last launch
     roof = roofline(kind, args.precision, N, M, T, w.T_use, B, P, kernel_ms, steady_lane_steps=64 * steady_ws)
     out_host = d_out.cpu().numpy()
+    if os.environ.get("YFM_BENCH_DUMP") and rank == 0:  # A/B runs (tools/ab_run.sh): the logliks, for a bitwise compare
+        np.save(os.environ["YFM_BENCH_DUMP"], out_host)
     # DNS, GNS5: the same workload with the full covariance recursion every step (YFM_DNS_STEADY=0), beside the
     # default — the steady state must not change a loglik by more than rounding (tests/test_gpu_steady.py)
     steady = None

@@ -34,6 +34,26 @@ namespace yfm {
 
 constexpr int kBlock = 256;  // 4 waves: one per SIMD of a CU
 constexpr int kTC = 64;  // panel columns per LDS chunk (DNS; GNS5 and the pipelined DNS blocks keep 32 for LDS)
+// Look-ahead MFMA blocks (DNS steady state, round 5): a steady block issues the NEXT block's 64 Z'ỹ MFMAs before
+// its own 16 mean updates and stores their results after them, into the other of two scratch buffers — the
+// accumulator read-out, the LDS writes and their landing no longer sit between a block's MFMAs and its first step
+// (the store tail, ≈ 1,100 cycles per block).  FP64 MFMA and FP64 VALU share the pipe, so the order costs no
+// arithmetic; the price is the second buffer (32-column panel chunks) and 64 AGPRs live across the steady steps.
+#ifndef YFM_DNS_SIGMA  // 0: the 16×16×4 D tiles stored as four 8-byte LDS writes per tile (rounds 1–4)
+#define YFM_DNS_SIGMA 1
+#endif
+#ifndef YFM_EARLY_CHUNKS  // 0: the first two panel chunks loaded after the setup, one round trip each (round 4)
+#define YFM_EARLY_CHUNKS 1
+#endif
+#ifndef YFM_MIDBLOCK_STEADY  // 0: a block that starts with the full recursion runs it to the block's end (round 4)
+#define YFM_MIDBLOCK_STEADY 1
+#endif
+#ifndef YFM_AF_IN_AGPR
+#define YFM_AF_IN_AGPR 1
+#endif
+#ifndef YFM_DNS_LOOKAHEAD
+#define YFM_DNS_LOOKAHEAD 0
+#endif
 constexpr bool kMfma4 = true;   // GNS5 Z'ỹ on v_mfma_f64_4x4x4_4b_f64 (DNS keeps v_mfma_f64_16x16x4_f64)
 constexpr bool kZBasis = true;  // GNS5 fragments e = 1 − e^{−λm} against (ỹ, ỹ/m): see the kernel
 #ifndef YFM_PIPE_VALU
@@ -147,7 +167,8 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   // panel columns per LDS chunk: 64 for DNS (a chunk rotation, with its two block barriers, every 64 steps
   // instead of 32: 0.2040 → 0.2022 ms at config 2, profiles/r4/ab23/); 32 where the LDS is taken by GNS5's
   // z̃ scratch or the pipelined block's second buffer
-  constexpr int TC = (M == 3 && !PIPE_) ? kTC : 32;
+  constexpr bool LA_ = YFM_DNS_LOOKAHEAD && STEADY_ && !RECORD && M == 3 && !PIPE_ && (NP <= 32);
+  constexpr int TC = (M == 3 && !PIPE_ && !LA_) ? kTC : 32;
   constexpr bool USE_MFMA_ = (M - 1 == 2 || M - 1 == 4) && (NP <= 32);
   // frozen-covariance steady state (FixedZFilter): the loglik-mode DNS instantiation
   // with STEADY_ (the plain instantiation is the full recursion, YFM_DNS_STEADY=0)
@@ -179,7 +200,8 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   // updates — the matrix pipe and the VALU then work side by side instead of one after the other — into
   // a second scratch buffer per wave (2 × 16.6 KB per wave: 151.5 KB of LDS at NP = 32)
   constexpr bool PIPE = PIPE_ && STEADY && NZ == 2 && !ZB;
-  constexpr int NBUF = PIPE ? 2 : 1;
+  constexpr bool LA = LA_ && STEADY && NZ == 2 && !ZB;
+  constexpr int NBUF = (PIPE || LA) ? 2 : 1;
   static_assert(NZ == 2 * LEAD, "loading columns come in (S, C) pairs per gamma");
   static_assert(NP % 2 == 0, "double2 panel reads");
   static_assert(TC % TB == 0, "MFMA blocks tile the panel chunk");
@@ -199,6 +221,34 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   const bool live = b < B;
   const int bb = live ? b : (B - 1);
   const int nobs = T_use ? T_use[bb] : T;
+
+  // panel chunk loads (PER doubles per thread; LDS holds chunks c and c+1 while chunk c is processed)
+  auto load_into = [&](double* dst, int c) {
+    const size_t base = (size_t)c * CH;
+    const size_t lim = (size_t)T * LDP;
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+      const int e = r * kBlock + tid;
+      const size_t g = base + e;
+      dst[r] = (e < CH && g < lim) ? panel[g] : 0.0;
+    }
+  };
+  auto store_from = [&](const double* src, double* buf) {
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+      const int e = r * kBlock + tid;
+      if (e < CH) buf[e] = src[r];
+    }
+  };
+  // EARLY: chunks 0 and 1 issued before the setup, so their HBM latency hides under the θ decode and the
+  // loadings instead of two serial round trips after it (stored to LDS where the staging starts below)
+  constexpr bool MID = YFM_MIDBLOCK_STEADY != 0;
+  constexpr bool EARLY = YFM_EARLY_CHUNKS && M == 3 && NP <= 32;  // GNS5 and NP > 32 spill with the 2·PER registers
+  double pre0[EARLY ? PER : 1], pre1[EARLY ? PER : 1];
+  if constexpr (EARLY) {
+    load_into(pre0, 0);
+    load_into(pre1, 1);
+  }
 
   if (tid == 0) s_nobs_max = 0;
   if constexpr (ZB) {
@@ -284,9 +334,14 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   asm volatile("" ::"v"(G[1][2]));
   const long long ph_s2 = __builtin_readcyclecounter();
 #endif
-  // MFMA A fragments: tile r, k-step kk — lane l holds Z of pair p = 16r + (l & 15)
-  // (candidate p >> 1 of this wave, column p & 1) at maturity 4kk + (l >> 4).
+  // MFMA A fragments: tile r, k-step kk — lane l holds Z of pair p = 16r + σ(l & 15)
+  // (candidate p / NZ of this wave, column p % NZ) at maturity 4kk + (l >> 4).
   // Gathered once through the wave's scratch, 16 candidates at a time.
+  // σ (the 16×16×4 form only): row i = g + 4q of a tile holds pair 16r + 4g + q, so the four D values a lane
+  // holds (rows g, g+4, g+8, g+12 of one step) are four consecutive pairs — two 16-byte LDS stores per tile
+  // instead of four 8-byte ones, and still one candidate's z̃ in consecutive doubles for the step reads
+  constexpr bool SIGMA = YFM_DNS_SIGMA && USE_MFMA && !ZB && !(kMfma4 && NZ == 4);
+  auto sigma = [](int i) { return SIGMA ? 4 * (i & 3) + (i >> 2) : i; };
   double Af[USE_MFMA ? NRTA : 1][USE_MFMA ? NK : 1];
   double rlam[LEAD];  // 1/λ_l (z-basis fragments)
 #pragma unroll
@@ -323,7 +378,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int r = h * HT; r < (h + 1) * HT; ++r) {
-        const int pr = 16 * r + (lane & 15) - h * 32 * RPC;  // pair index within this half
+        const int pr = 16 * r + sigma(lane & 15) - h * 32 * RPC;  // pair index within this half
 #pragma unroll
         for (int kk = 0; kk < NK; ++kk) Af[r][kk] = st[pr * ZS + 4 * kk + (lane >> 4)];
       }
@@ -374,32 +429,33 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
 
   // ---- panel staging: LDS holds chunks c and c+1 while chunk c is processed ----------
   double pre[PER];
-  auto load_chunk = [&](int c) {
-    const size_t base = (size_t)c * CH;
-    const size_t lim = (size_t)T * LDP;
-#pragma unroll
-    for (int r = 0; r < PER; ++r) {
-      const int e = r * kBlock + tid;
-      const size_t g = base + e;
-      pre[r] = (e < CH && g < lim) ? panel[g] : 0.0;
-    }
-  };
-  auto store_chunk = [&](double* buf) {
-#pragma unroll
-    for (int r = 0; r < PER; ++r) {
-      const int e = r * kBlock + tid;
-      if (e < CH) buf[e] = pre[r];
-    }
-  };
+  auto load_chunk = [&](int c) { load_into(pre, c); };
+  auto store_chunk = [&](double* buf) { store_from(pre, buf); };
   if (nsteps > 0) {
-    load_chunk(0);
-    store_chunk(sh[0]);
-    load_chunk(1);
-    store_chunk(sh[1]);
+    if constexpr (EARLY) {
+      store_from(pre0, sh[0]);
+      store_from(pre1, sh[1]);
+    } else {
+      load_chunk(0);
+      store_chunk(sh[0]);
+      load_chunk(1);
+      store_chunk(sh[1]);
+    }
     __syncthreads();
     load_chunk(2);
   }
   auto col_of = [&](int t) -> const double* { return sh[(t / TC) & 1] + (t % TC) * LDP; };
+  // a 16×16×4 D tile into a scratch buffer: lane l holds step l & 15, pairs 16r + 4(l >> 4) + q (σ above)
+  auto store_tile = [&](double* dst, int r, const yfm_double4& a) {
+    if constexpr (SIGMA) {
+      double* d = dst + (lane & 15) * SS + 16 * r + 4 * (lane >> 4);
+      *reinterpret_cast<double2*>(d) = make_double2(a[0], a[1]);
+      *reinterpret_cast<double2*>(d + 2) = make_double2(a[2], a[3]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dst[(lane & 15) * SS + 16 * r + (lane >> 4) + 4 * q] = a[q];
+    }
+  };
 
   // one filter step given z̃_t (zc), (ȳ, ỹ'ỹ) and (nanflag, y'y) of column t
   auto do_step = [&](int t, const double (&zc)[NZ], double2 yb_c, double2 meta_c) {
@@ -437,10 +493,18 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
       const long long ph_a = __builtin_readcyclecounter();
 #endif
       if constexpr (STEADY) f.prepare_bound();
+      if constexpr (YFM_AF_IN_AGPR && SIGMA) {
+        // the A fragments stay in AGPRs, where the 16×16×4 MFMA reads them as its A operand (left to itself the
+        // allocator copies each one to a VGPR before its MFMA: 128 v_accvgpr_read per block)
+#pragma unroll
+        for (int r = 0; r < NRTA; ++r)
+#pragma unroll
+          for (int kk = 0; kk < NK; ++kk) asm volatile("" : "+a"(Af[r][kk]));
+      }
 #ifdef YFM_PHASE_PROBE
       long long ph_a2 = __builtin_readcyclecounter(), ph_a3 = ph_a2;
 #endif
-      double* scr = scratch[wave][PIPE ? buf : 0];
+      double* scr = scratch[wave][(PIPE || LA) ? buf : 0];
       // ---- z̃ for steps t0 .. t0+15 of all 64 candidates: NRT·NK MFMAs ----
       const double* cb = col_of(t0);  // TB consecutive columns of one chunk
       // the block's NaN flags, one column per lane, read before the MFMAs so the steady-block vote after them
@@ -531,16 +595,13 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
 #pragma unroll
             for (int r = 0; r < RGN; ++r)
               acc[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(Af[r0 + r][kk], bvk[kk], acc[r], 0, 0, 0);
-          // D[row = pair][col = step]: lane l holds step l & 15, pairs 16r + (l >> 4) + 4q
+          // D[row][col = step]: lane l holds step l & 15, rows (l >> 4) + 4q = pairs 16r + 4(l >> 4) + q
 #ifdef YFM_PROBE_NOWRITE  // timing probe: results kept in registers, never stored (the block reads stale z̃)
 #pragma unroll
           for (int r = 0; r < RGN; ++r) asm volatile("" ::"a"(acc[r]));
 #else
 #pragma unroll
-          for (int r = 0; r < RGN; ++r)
-#pragma unroll
-            for (int q4 = 0; q4 < 4; ++q4)
-              scr[(lane & 15) * SS + 16 * (r0 + r) + (lane >> 4) + 4 * q4] = acc[r][q4];
+          for (int r = 0; r < RGN; ++r) store_tile(scr, r0 + r, acc[r]);
 #endif
         }
 #ifdef YFM_PROBE_MFMA2X  // timing probe: the block's MFMAs a second time, results discarded
@@ -587,6 +648,33 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
 #ifdef YFM_PHASE_PROBE
       const long long ph_c = __builtin_readcyclecounter();
 #endif
+      // LA: the next block's Z'ỹ MFMAs, issued now, stored after this block's steady steps (into the other buffer)
+      bool la_next = false;
+      yfm_double4 la_acc[LA ? NRT : 1];
+      if constexpr (LA) {
+        if (blk_steady && tend == TB && t0 + TB < nsteps) {
+          la_next = true;
+          const double* nb = col_of(t0 + TB);  // resident: the next 16 columns are in this or the next chunk
+          double bvn[NK];
+#pragma unroll
+          for (int kk = 0; kk < NK; ++kk) {
+            const int m = 4 * kk + (lane >> 4);
+            bvn[kk] = (m < NP) ? nb[(lane & 15) * LDP + m] : 0.0;
+          }
+#pragma unroll
+          for (int r = 0; r < NRT; ++r) la_acc[r] = yfm_double4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int kk = 0; kk < NK; ++kk)
+#pragma unroll
+            for (int r = 0; r < NRT; ++r)
+              la_acc[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(Af[r][kk], bvn[kk], la_acc[r], 0, 0, 0);
+          // the first half of the tiles now (their MFMAs finished while the second half issued); the second
+          // half after the steps, so only 32 accumulator registers stay live across them
+          double* scn = scratch[wave][buf ^ 1];
+#pragma unroll
+          for (int r = 0; r < NRT / 2; ++r) store_tile(scn, r, la_acc[r]);
+        }
+      }
       // step operands for tt are read one step ahead (hides the LDS latency at 1 wave/SIMD)
       auto read_z = [&](int tt, double (&z)[NZ]) {  // this lane's pairs NZ·lane .. NZ·lane + NZ − 1
         const double* sp = scr + tt * SS + NZ * lane;
@@ -619,6 +707,15 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
         do_step(t, zc_, yb_, meta_);
         record(t);
         rotate(t);
+      };
+      // the mean update only, with the cached factors of S (bitwise the full step's values for a frozen lane);
+      // operands read one step ahead as in `half`
+      auto shalf = [&](int tt, const double (&zc_)[NZ], double2 yb_, double (&zn_)[NZ], double2& ybn_) {
+        const int tn = min(tt + 1, TB - 1);
+        read_z(tn, zn_);
+        ybn_ = *reinterpret_cast<const double2*>(cb + tn * LDP + NP);
+        f.steady_step(zc_, yb_);
+        rotate(t0 + tt);
       };
       bool have_next = false;
       if constexpr (PIPE) {
@@ -654,11 +751,8 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
               pa0 = __builtin_amdgcn_mfma_f64_16x16x4f64(Af[rp][kk], bv, pa0, 0, 0, 0);
               pa1 = __builtin_amdgcn_mfma_f64_16x16x4f64(Af[rp + 1][kk], bv, pa1, 0, 0, 0);
               if (kk == NK - 1) {
-#pragma unroll
-                for (int q4 = 0; q4 < 4; ++q4) {
-                  scn[(lane & 15) * SS + 16 * rp + (lane >> 4) + 4 * q4] = pa0[q4];
-                  scn[(lane & 15) * SS + 16 * (rp + 1) + (lane >> 4) + 4 * q4] = pa1[q4];
-                }
+                store_tile(scn, rp, pa0);
+                store_tile(scn, rp + 1, pa1);
               }
             }
             f.steady_step(zq[cur], ybq[cur]);
@@ -688,15 +782,6 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
       }
       if constexpr (STEADY) {
         if (blk_steady && !have_next) {
-          // the mean update only, with the cached factors of S (bitwise the full step's values for a
-          // frozen lane); operands read one step ahead as in `half`
-          auto shalf = [&](int tt, const double (&zc_)[NZ], double2 yb_, double (&zn_)[NZ], double2& ybn_) {
-            const int tn = min(tt + 1, TB - 1);
-            read_z(tn, zn_);
-            ybn_ = *reinterpret_cast<const double2*>(cb + tn * LDP + NP);
-            f.steady_step(zc_, yb_);
-            rotate(t0 + tt);
-          };
           if (tend == TB) {
             // a whole block: the 16 steps unrolled into one basic block (no loop control or operand copies;
             // the chunk rotation, which only the block's last step can trigger, after it): 0.2114 → 0.2042 ms
@@ -714,6 +799,13 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
               ybq[nx] = *reinterpret_cast<const double2*>(cb + tn * LDP + NP);
               f.steady_step(zq[cur], ybq[cur]);
             }
+            if constexpr (LA) {
+              if (la_next) {  // the next block's z̃ (the D layout of the block form above), other buffer
+                double* scn = scratch[wave][buf ^ 1];
+#pragma unroll
+                for (int r = NRT / 2; r < NRT; ++r) store_tile(scn, r, la_acc[r]);
+              }
+            }
             rotate(t0 + TB - 1);
           } else {
             int tt = 0;
@@ -729,6 +821,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
       }
       if (!blk_steady) {
         int tt = 0;
+        bool rest_steady = false;  // MID: the rest of this block runs in the steady loop
         for (; tt + 1 < tend; tt += 2) {
           half(tt, zc, yb, meta, zn, ybn, metan);
           half(tt + 1, zn, ybn, metan, zc, yb, meta);
@@ -736,10 +829,44 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
             // mid-block as well: lanes may freeze within this block (without it the config-2 steady share
             // drops 0.973 → 0.947, 0.226 → 0.234 ms; profiles/r4/exp1/)
             if (tt == TB / 2 - 2) f.prepare_bound();
+            if constexpr (MID) {
+              // from the block's second half on, at every step pair: once every lane is frozen (the wave
+              // vote of the block's end, taken early) and the rest of the block is data steps of every lane
+              // with no NaN column, the remaining steps run as steady steps — the first block's waves freeze
+              // at steps 10–14 (tools/steady_rule.py), so up to 6 of its 16 full steps become steady ones.
+              // The lanes' values are bitwise the same either way (the steady step is the full step of a
+              // frozen lane); only which loop runs them changes
+              const int r0 = tt + 2;
+              if (r0 >= TB / 2 && r0 < tend && t0 + tend <= wave_min_data) {
+                const bool nan_rest = (lane >= r0) && (lane < tend) && (col_flag != 0.0);
+                if (!__any(nan_rest)) {
+                  f.wave_freeze(live && !defer && f.init_ok && t0 + tend <= my_steps);
+                  if (f.wave_frozen) {  // wave-uniform (wave_freeze votes)
+                    rest_steady = true;
+                    tt = r0;
+                    break;
+                  }
+                }
+              }
+            }
           }
         }
-        if (tt < tend) half(tt, zc, yb, meta, zn, ybn, metan);
-        if constexpr (STEADY) f.wave_freeze(live && !defer && f.init_ok && t0 + tend <= my_steps);
+        if constexpr (STEADY && MID) {
+          if (rest_steady) {  // step tt's operands are in (zc, yb): read ahead by the last `half`
+            const int n = tend - tt;
+            for (; tt + 1 < tend; tt += 2) {
+              shalf(tt, zc, yb, zn, ybn);
+              shalf(tt + 1, zn, ybn, zc, yb);
+            }
+            if (tt < tend) shalf(tt, zc, yb, zn, ybn);
+            steady_steps += n;
+            f.count_steady(n);
+          }
+        }
+        if (!rest_steady) {
+          if (tt < tend) half(tt, zc, yb, meta, zn, ybn, metan);
+          if constexpr (STEADY) f.wave_freeze(live && !defer && f.init_ok && t0 + tend <= my_steps);
+        }
       }
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();  // scratch reads done before the next block's writes
@@ -760,6 +887,10 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
       if constexpr (PIPE) {
         buf ^= 1;
         have_z = have_next;
+      }
+      if constexpr (LA) {
+        have_z = la_next;
+        if (la_next) buf ^= 1;
       }
     }
     if constexpr (STEADY) {
