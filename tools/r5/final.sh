@@ -43,7 +43,17 @@ for c in 2 3 4 5; do
   timeout -k 10 300 python -u bench.py --config $c --steps $steps --warmup 5 > "$OUT/bench_c$c.json" 2> "$OUT/bench_c$c.err"; ok
   python3 -c "import json; d=json.load(open('$OUT/bench_c$c.json')); r=d['roofline']; print('c$c', d['value'], r['kernel_ms'], r['frac'], r['traffic'])"
 done
+# config 3 at the estimator's batch sizes (B ∈ {1, 1,024, 16,384}): kernel statistics + bench line
+for B in 1 1024; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt_c3_B$B" -o kt --output-format csv -- \
+    python3 bench.py --config 3 --batch $B --steps 20 --warmup 3 --no-cpu-baseline --no-host-rate > "$OUT/kt_c3_B$B.json" 2> "$OUT/kt_c3_B$B.err"; ok
+  find "$OUT/kt_c3_B$B" -name "*kernel_trace.csv" -delete
+  timeout -k 10 300 python -u bench.py --config 3 --batch $B --steps 30 --warmup 5 > "$OUT/bench_c3_B$B.json" 2> "$OUT/bench_c3_B$B.err"; ok
+  python3 -c "import json; d=json.load(open('$OUT/bench_c3_B$B.json')); print('c3 B=$B', d['value'], d['roofline']['kernel_ms'])"
+done
 timeout -k 10 300 python -u tools/bench_estimate.py > "$OUT/bench_estimate.json" 2> "$OUT/bench_estimate.err"; ok
+timeout -k 10 400 python -u tools/bench_estimate.py --model tvl --windows 240 > "$OUT/bench_estimate_tvl.json" 2> "$OUT/bench_estimate_tvl.err"; ok
+timeout -k 10 60 ./tools/mfma_block_probe > "$OUT/mfma_block_probe.txt" 2>&1; ok
 timeout -k 10 300 bash tools/agpr_spill_repro/run.sh > "$OUT/agpr_repro.log" 2>&1; ok
 timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/driver_cmd.json" 2> "$OUT/driver_cmd.err"; ok
 python3 -c "import json; d=json.load(open('$OUT/driver_cmd.json')); print('driver cmd', d['value'], d['ms_per_step'])"

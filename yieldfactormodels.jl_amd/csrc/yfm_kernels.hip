@@ -51,6 +51,9 @@ constexpr int kTC = 64;  // panel columns per LDS chunk (DNS; GNS5 and the pipel
 #ifndef YFM_AF_IN_AGPR
 #define YFM_AF_IN_AGPR 1
 #endif
+#ifndef YFM_AF_AGPR_GNS
+#define YFM_AF_AGPR_GNS 1
+#endif
 #ifndef YFM_DNS_LOOKAHEAD
 #define YFM_DNS_LOOKAHEAD 0
 #endif
@@ -243,6 +246,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   // EARLY: chunks 0 and 1 issued before the setup, so their HBM latency hides under the θ decode and the
   // loadings instead of two serial round trips after it (stored to LDS where the staging starts below)
   constexpr bool MID = YFM_MIDBLOCK_STEADY != 0;
+  constexpr bool AF_AGPR_GNS = YFM_AF_AGPR_GNS && M == 5;
   constexpr bool EARLY = YFM_EARLY_CHUNKS && M == 3 && NP <= 32;  // GNS5 and NP > 32 spill with the 2·PER registers
   double pre0[EARLY ? PER : 1], pre1[EARLY ? PER : 1];
   if constexpr (EARLY) {
@@ -493,7 +497,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
       const long long ph_a = __builtin_readcyclecounter();
 #endif
       if constexpr (STEADY) f.prepare_bound();
-      if constexpr (YFM_AF_IN_AGPR && SIGMA) {
+      if constexpr (YFM_AF_IN_AGPR && (SIGMA || AF_AGPR_GNS)) {
         // the A fragments stay in AGPRs, where the 16×16×4 MFMA reads them as its A operand (left to itself the
         // allocator copies each one to a VGPR before its MFMA: 128 v_accvgpr_read per block)
 #pragma unroll
