@@ -247,7 +247,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   // loadings instead of two serial round trips after it (stored to LDS where the staging starts below)
   constexpr bool MID = YFM_MIDBLOCK_STEADY != 0;
   constexpr bool AF_AGPR_GNS = YFM_AF_AGPR_GNS && M == 5;
-  constexpr bool EARLY = YFM_EARLY_CHUNKS && M == 3 && NP <= 32;  // GNS5 and NP > 32 spill with the 2·PER registers
+  constexpr bool EARLY = YFM_EARLY_CHUNKS != 0 && M == 3 && NP <= 32;  // GNS5 and NP > 32 spill with the 2·PER registers
   double pre0[EARLY ? PER : 1], pre1[EARLY ? PER : 1];
   if constexpr (EARLY) {
     load_into(pre0, 0);

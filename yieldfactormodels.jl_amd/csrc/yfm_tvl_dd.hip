@@ -37,6 +37,12 @@
 #define YFM_TVL_MOMENTS 0
 #endif
 
+// waves per SIMD the loglik kernel is compiled for (A/B builds: 2 caps it at 256 registers per lane, so that
+// L = 8 at config 3 runs two waves per SIMD)
+#ifndef YFM_TVL_DD_WAVES
+#define YFM_TVL_DD_WAVES 1
+#endif
+
 namespace yfm {
 
 namespace {
@@ -301,7 +307,7 @@ __global__ __launch_bounds__(64) void tvl_dd_colsum_kernel(const double* __restr
 }
 
 template <int L, bool RECORD>
-__global__ __launch_bounds__(kDdBlock) void tvl_dd_loglik_kernel(
+__global__ __launch_bounds__(kDdBlock, YFM_TVL_DD_WAVES) void tvl_dd_loglik_kernel(
     const double* __restrict__ rec, int B, const double* __restrict__ Y, const double* __restrict__ colsum,
     const double* __restrict__ prep, int ldp,
     int np, int T, int N, int TC, const double* __restrict__ mats, int K, const double* __restrict__ gap_d,
