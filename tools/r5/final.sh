@@ -3,7 +3,8 @@
 # config 2-5 the PMC passes (one counter group per run, each under a hard limit) with their per-kernel
 # summary, the rocprofv3 kernel statistics, and the bench line (which reads the PMC summary for
 # roofline.traffic), then the rolling re-estimation benchmark and the driver's own bench command.
-#   bash tools/r5/final.sh <outdir under gpurun_out/>      (SKIP_TESTS=1: no pytest/smoke)
+#   bash tools/r5/final.sh <outdir under gpurun_out/>      (SKIP_TESTS=1: no pytest/smoke; CONFIGS="2 3": those
+#   configurations only; SKIP_EXTRA=1: no small-B / estimator / probe / driver-command steps)
 set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-r5final}
@@ -20,7 +21,7 @@ if [ -z "$SKIP_TESTS" ]; then
   tail -1 "$OUT/smoke.log"
 fi
 declare -A EV=([2]=65536 [3]=16384 [4]=983040 [5]=1048576)
-for c in 2 3 4 5; do
+for c in ${CONFIGS:-2 3 4 5}; do
   P="$OUT/pmc_c$c"
   mkdir -p "$P"
   pass() { name=$1; shift
@@ -43,6 +44,7 @@ for c in 2 3 4 5; do
   timeout -k 10 300 python -u bench.py --config $c --steps $steps --warmup 5 > "$OUT/bench_c$c.json" 2> "$OUT/bench_c$c.err"; ok
   python3 -c "import json; d=json.load(open('$OUT/bench_c$c.json')); r=d['roofline']; print('c$c', d['value'], r['kernel_ms'], r['frac'], r['traffic'])"
 done
+[ -n "$SKIP_EXTRA" ] && exit 0
 # config 3 at the estimator's batch sizes (B ∈ {1, 1,024, 16,384}): kernel statistics + bench line
 for B in 1 1024; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt_c3_B$B" -o kt --output-format csv -- \
