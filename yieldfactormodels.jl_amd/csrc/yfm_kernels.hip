@@ -54,6 +54,9 @@ constexpr int kTC = 64;  // panel columns per LDS chunk (DNS; GNS5 and the pipel
 #ifndef YFM_AF_AGPR_GNS
 #define YFM_AF_AGPR_GNS 1
 #endif
+#ifndef YFM_STORE_INTERLEAVE
+#define YFM_STORE_INTERLEAVE 1
+#endif
 #ifndef YFM_DNS_LOOKAHEAD
 #define YFM_DNS_LOOKAHEAD 0
 #endif
@@ -345,6 +348,8 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   // holds (rows g, g+4, g+8, g+12 of one step) are four consecutive pairs — two 16-byte LDS stores per tile
   // instead of four 8-byte ones, and still one candidate's z̃ in consecutive doubles for the step reads
   constexpr bool SIGMA = YFM_DNS_SIGMA && USE_MFMA && !ZB && !(kMfma4 && NZ == 4);
+  // IL: the first row-tile group's stores interleaved with the second group's MFMAs (NP 29–32: one per k-step)
+  constexpr bool IL = YFM_STORE_INTERLEAVE && SIGMA && NRT == 2 * RGN && NK == 2 * RGN;
   auto sigma = [](int i) { return SIGMA ? 4 * (i & 3) + (i >> 2) : i; };
   double Af[USE_MFMA ? NRTA : 1][USE_MFMA ? NK : 1];
   double rlam[LEAD];  // 1/λ_l (z-basis fragments)
@@ -589,6 +594,35 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
         __builtin_amdgcn_s_waitcnt(0xc07f);
         ph_a3 = __builtin_readcyclecounter();
 #endif
+        if constexpr (IL) {
+          // the first group's 8 16-byte stores issued one per k-step of the second group's MFMAs (the wave
+          // issues them while the matrix pipe works) instead of back to back between the groups
+          yfm_double4 a1[RGN], a2[RGN];
+#pragma unroll
+          for (int r = 0; r < RGN; ++r) a1[r] = a2[r] = yfm_double4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int kk = 0; kk < NK; ++kk)
+#pragma unroll
+            for (int r = 0; r < RGN; ++r)
+              a1[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(Af[r][kk], bvk[kk], a1[r], 0, 0, 0);
+#pragma unroll
+          for (int kk = 0; kk < NK; ++kk) {
+#pragma unroll
+            for (int r = 0; r < RGN; ++r)
+              a2[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(Af[RGN + r][kk], bvk[kk], a2[r], 0, 0, 0);
+            const int r1 = kk >> 1, h = kk & 1;
+            double* d = scr + (lane & 15) * SS + 16 * r1 + 4 * (lane >> 4) + 2 * h;
+            *reinterpret_cast<double2*>(d) = make_double2(a1[r1][2 * h], a1[r1][2 * h + 1]);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, RGN * NK, 0);  // the first group's MFMAs
+#pragma unroll
+          for (int kk = 0; kk < NK; ++kk) {
+            __builtin_amdgcn_sched_group_barrier(0x008, RGN, 0);  // a k-step of the second group
+            __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);    // one store of the first
+          }
+#pragma unroll
+          for (int r = 0; r < RGN; ++r) store_tile(scr, RGN + r, a2[r]);
+        } else {
 #pragma unroll
         for (int r0 = 0; r0 < NRT; r0 += RGN) {
           yfm_double4 acc[RGN];
@@ -607,6 +641,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
 #pragma unroll
           for (int r = 0; r < RGN; ++r) store_tile(scr, r0 + r, acc[r]);
 #endif
+        }
         }
 #ifdef YFM_PROBE_MFMA2X  // timing probe: the block's MFMAs a second time, results discarded
         double bvq[NK];  // opaque copies: the second pass must not be merged with the first
