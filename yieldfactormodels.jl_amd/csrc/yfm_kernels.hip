@@ -350,6 +350,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   constexpr bool SIGMA = YFM_DNS_SIGMA && USE_MFMA && !ZB && !(kMfma4 && NZ == 4);
   // IL: the first row-tile group's stores interleaved with the second group's MFMAs (NP 29–32: one per k-step)
   constexpr bool IL = YFM_STORE_INTERLEAVE && SIGMA && NRT == 2 * RGN && NK == 2 * RGN;
+  constexpr bool IL5 = YFM_STORE_INTERLEAVE && ZB && NK == NRTA;  // GNS5: the same across step pairs
   auto sigma = [](int i) { return SIGMA ? 4 * (i & 3) + (i >> 2) : i; };
   double Af[USE_MFMA ? NRTA : 1][USE_MFMA ? NK : 1];
   double rlam[LEAD];  // 1/λ_l (z-basis fragments)
@@ -521,6 +522,51 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
       const double col_flag = cb[min(lane, TB - 1) * LDP + NP + 2];
       if (have_z) {
         // (PIPE) already in scratch[wave][buf]
+      } else if constexpr (ZB && IL5) {
+        // as below, software-pipelined over the step pairs: step pair sp − 1's 8 results are stored one per
+        // k-step of step pair sp's MFMAs (the wave issues the stores while the matrix pipe works)
+        double accp[NRTA];
+#pragma unroll
+        for (int sp = 0; sp <= TB / 2; ++sp) {
+          double acc[NRTA];
+          if (sp < TB / 2) {
+            double bv[NK];
+#pragma unroll
+            for (int kk = 0; kk < NK; ++kk) {
+              const int m = 4 * kk + (lane >> 4);
+              const double y = (m < NP) ? cb[(2 * sp + ((lane & 3) >> 1)) * LDP + m] : 0.0;
+              bv[kk] = (lane & 1) ? y * s_rm[m < NP ? m : 0] : y;
+            }
+#pragma unroll
+            for (int r = 0; r < NRTA; ++r) acc[r] = 0.0;
+#pragma unroll
+            for (int kk = 0; kk < NK; ++kk) {
+#pragma unroll
+              for (int r = 0; r < NRTA; ++r)
+                acc[r] = __builtin_amdgcn_mfma_f64_4x4x4f64(Af[r][kk], bv[kk], acc[r], 0, 0, 0);
+              if (sp > 0)
+                scr[(2 * (sp - 1) + ((lane & 3) >> 1)) * SS + 2 * (16 * kk + 4 * ((lane >> 2) & 3) + (lane >> 4)) +
+                    (lane & 1)] = accp[kk];
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < NRTA; ++r)
+              scr[(2 * (sp - 1) + ((lane & 3) >> 1)) * SS + 2 * (16 * r + 4 * ((lane >> 2) & 3) + (lane >> 4)) +
+                  (lane & 1)] = accp[r];
+          }
+          if (sp < TB / 2) {
+#pragma unroll
+            for (int r = 0; r < NRTA; ++r) accp[r] = acc[r];
+          }
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, NRTA * NK, 0);  // step pair 0's MFMAs
+#pragma unroll
+        for (int sp = 1; sp < TB / 2; ++sp)
+#pragma unroll
+          for (int kk = 0; kk < NK; ++kk) {
+            __builtin_amdgcn_sched_group_barrier(0x008, NRTA, 0);  // a k-step of step pair sp
+            __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);     // one store of step pair sp − 1
+          }
       } else if constexpr (ZB) {
         // rows: pair 16r + 4blk + i = (candidate, γ index); columns j of step pair sp: step
         // 2sp + (j >> 1), ỹ (j even) or ỹ/m (j odd)
