@@ -55,7 +55,7 @@ constexpr int kTC = 64;  // panel columns per LDS chunk (DNS; GNS5 and the pipel
 #define YFM_AF_AGPR_GNS 1
 #endif
 #ifndef YFM_STORE_INTERLEAVE
-#define YFM_STORE_INTERLEAVE 1
+#define YFM_STORE_INTERLEAVE 2  // 1: two tile groups (4, 4); 2: three (4, 2, 2), the default; 0: stores after each group
 #endif
 #ifndef YFM_DNS_LOOKAHEAD
 #define YFM_DNS_LOOKAHEAD 0
@@ -640,7 +640,54 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
         __builtin_amdgcn_s_waitcnt(0xc07f);
         ph_a3 = __builtin_readcyclecounter();
 #endif
-        if constexpr (IL) {
+        if constexpr (IL && YFM_STORE_INTERLEAVE == 2) {
+          // three groups of 4, 2, 2 tiles: the first group's 8 stores during the second group's MFMAs, the
+          // second's 4 during the third's, so only the last 2 tiles' 4 stores trail the block
+          constexpr int H = RGN / 2;
+          yfm_double4 a1[RGN], a2[H], a3[H];
+#pragma unroll
+          for (int r = 0; r < RGN; ++r) a1[r] = yfm_double4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int r = 0; r < H; ++r) a2[r] = a3[r] = yfm_double4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int kk = 0; kk < NK; ++kk)
+#pragma unroll
+            for (int r = 0; r < RGN; ++r)
+              a1[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(Af[r][kk], bvk[kk], a1[r], 0, 0, 0);
+#pragma unroll
+          for (int kk = 0; kk < NK; ++kk) {
+#pragma unroll
+            for (int r = 0; r < H; ++r)
+              a2[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(Af[RGN + r][kk], bvk[kk], a2[r], 0, 0, 0);
+            const int r1 = kk >> 1, h = kk & 1;
+            double* d = scr + (lane & 15) * SS + 16 * r1 + 4 * (lane >> 4) + 2 * h;
+            *reinterpret_cast<double2*>(d) = make_double2(a1[r1][2 * h], a1[r1][2 * h + 1]);
+          }
+#pragma unroll
+          for (int kk = 0; kk < NK; ++kk) {
+#pragma unroll
+            for (int r = 0; r < H; ++r)
+              a3[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(Af[RGN + H + r][kk], bvk[kk], a3[r], 0, 0, 0);
+            if (kk & 1) {
+              const int r2 = kk >> 2, h = (kk >> 1) & 1;
+              double* d = scr + (lane & 15) * SS + 16 * (RGN + r2) + 4 * (lane >> 4) + 2 * h;
+              *reinterpret_cast<double2*>(d) = make_double2(a2[r2][2 * h], a2[r2][2 * h + 1]);
+            }
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, RGN * NK, 0);  // the first group's MFMAs
+#pragma unroll
+          for (int kk = 0; kk < NK; ++kk) {
+            __builtin_amdgcn_sched_group_barrier(0x008, H, 0);  // a k-step of the second group
+            __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // one store of the first
+          }
+#pragma unroll
+          for (int kk = 0; kk < NK; ++kk) {
+            __builtin_amdgcn_sched_group_barrier(0x008, H, 0);  // a k-step of the third group
+            if (kk & 1) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // one store of the second
+          }
+#pragma unroll
+          for (int r = 0; r < H; ++r) store_tile(scr, RGN + H + r, a3[r]);
+        } else if constexpr (IL) {
           // the first group's 8 16-byte stores issued one per k-step of the second group's MFMAs (the wave
           // issues them while the matrix pipe works) instead of back to back between the groups
           yfm_double4 a1[RGN], a2[RGN];
