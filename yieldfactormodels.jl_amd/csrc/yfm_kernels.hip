@@ -57,6 +57,9 @@ constexpr int kTC = 64;  // panel columns per LDS chunk (DNS; GNS5 and the pipel
 #ifndef YFM_STORE_INTERLEAVE
 #define YFM_STORE_INTERLEAVE 2  // 1: two tile groups (4, 4); 2: three (4, 2, 2), the default; 0: stores after each group
 #endif
+#ifndef YFM_ROTATE_LATE  // a steady block's chunk rotation at the next block's start (0: after its steps, round 4)
+#define YFM_ROTATE_LATE 1
+#endif
 #ifndef YFM_DNS_LOOKAHEAD
 #define YFM_DNS_LOOKAHEAD 0
 #endif
@@ -249,6 +252,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   // EARLY: chunks 0 and 1 issued before the setup, so their HBM latency hides under the θ decode and the
   // loadings instead of two serial round trips after it (stored to LDS where the staging starts below)
   constexpr bool MID = YFM_MIDBLOCK_STEADY != 0;
+  constexpr bool RL = YFM_ROTATE_LATE != 0;
   constexpr bool AF_AGPR_GNS = YFM_AF_AGPR_GNS && M == 5;
   constexpr bool EARLY = YFM_EARLY_CHUNKS != 0 && M == 3 && NP <= 32;  // GNS5 and NP > 32 spill with the 2·PER registers
   double pre0[EARLY ? PER : 1], pre1[EARLY ? PER : 1];
@@ -496,7 +500,14 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
                                     // atomic would put its latency on the next global load's wait)
     int buf = 0;          // PIPE: this block's scratch buffer
     bool have_z = false;  // PIPE: this block's z̃ were formed during the previous (steady) block
+    int rot_t = -1;  // RL: a whole steady block's chunk rotation, deferred to the next block's start
     for (int t0 = 0; t0 < nsteps; t0 += TB) {
+      if constexpr (RL) {
+        if (rot_t >= 0) {
+          rotate(rot_t);
+          rot_t = -1;
+        }
+      }
       // the freeze rule's contraction bound, once per lane, at a block boundary before the block's MFMA
       // accumulators are live (FixedZFilter::prepare_bound)
 #ifdef YFM_PHASE_PROBE
@@ -938,7 +949,13 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
                 for (int r = NRT / 2; r < NRT; ++r) store_tile(scn, r, la_acc[r]);
               }
             }
-            rotate(t0 + TB - 1);
+            // RL: the rotation at the next block's start instead — with its barrier after the steps the compiler
+            // sinks the steps' arithmetic below it and issues all 32 operand reads up front (128 registers)
+            if constexpr (RL) {
+              rot_t = ((t0 + TB) % TC == 0) ? t0 + TB - 1 : -1;
+            } else {
+              rotate(t0 + TB - 1);
+            }
           } else {
             int tt = 0;
             for (; tt + 1 < tend; tt += 2) {
@@ -1024,6 +1041,9 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
         have_z = la_next;
         if (la_next) buf ^= 1;
       }
+    }
+    if constexpr (RL) {
+      if (rot_t >= 0) rotate(rot_t);  // every wave passes the same barriers
     }
     if constexpr (STEADY) {
       if (lane == 0 && steady_steps) atomicAdd(&flags[4], steady_steps);  // yfm_last_batch_steady
