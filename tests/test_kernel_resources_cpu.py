@@ -20,7 +20,7 @@ BUDGETS = {
     # the same with the full recursion (YFM_DNS_STEADY=0, the steady-vs-full gate)
     "fixedz_loglik_kernelILi30ELi3ELi1ELb0ELb0ELb0ELb0E": 0,
     # config 5: GNS5, NP = 30, full recursion
-    "fixedz_loglik_kernelILi30ELi5ELi2ELb0ELb0ELb0ELb0E": 16,
+    "fixedz_loglik_kernelILi30ELi5ELi2ELb0ELb0ELb0ELb0E": 0,
     # config 3: certified TVλ at L = 4
     "tvl_dd_loglik_kernelILi4ELb0E": 0,
 }

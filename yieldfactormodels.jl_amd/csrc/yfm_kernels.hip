@@ -58,7 +58,7 @@ constexpr int kTC = 64;  // panel columns per LDS chunk (DNS; GNS5 and the pipel
 #define YFM_STORE_INTERLEAVE 2  // 1: two tile groups (4, 4); 2: three (4, 2, 2), the default; 0: stores after each group
 #endif
 #ifndef YFM_ROTATE_LATE  // a steady block's chunk rotation at the next block's start (0: after its steps, round 4)
-#define YFM_ROTATE_LATE 1
+#define YFM_ROTATE_LATE 2  // 1: only a whole steady block's; 2: every block-end rotation (default)
 #endif
 #ifndef YFM_DNS_LOOKAHEAD
 #define YFM_DNS_LOOKAHEAD 0
@@ -253,6 +253,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   // loadings instead of two serial round trips after it (stored to LDS where the staging starts below)
   constexpr bool MID = YFM_MIDBLOCK_STEADY != 0;
   constexpr bool RL = YFM_ROTATE_LATE != 0;
+  constexpr bool RL2 = YFM_ROTATE_LATE == 2;  // every path's block-end rotation deferred (full steps too)
   constexpr bool AF_AGPR_GNS = YFM_AF_AGPR_GNS && M == 5;
   constexpr bool EARLY = YFM_EARLY_CHUNKS != 0 && M == 3 && NP <= 32;  // GNS5 and NP > 32 spill with the 2·PER registers
   double pre0[EARLY ? PER : 1], pre1[EARLY ? PER : 1];
@@ -849,7 +850,11 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
         metan_ = *reinterpret_cast<const double2*>(cb + tn * LDP + NP + 2);
         do_step(t, zc_, yb_, meta_);
         record(t);
-        rotate(t);
+        if constexpr (RL2) {
+          if ((t + 1) % TC == 0) rot_t = t;  // (RL2) deferred to the next block's start, as a steady block's
+        } else {
+          rotate(t);
+        }
       };
       // the mean update only, with the cached factors of S (bitwise the full step's values for a frozen lane);
       // operands read one step ahead as in `half`
@@ -858,7 +863,11 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
         read_z(tn, zn_);
         ybn_ = *reinterpret_cast<const double2*>(cb + tn * LDP + NP);
         f.steady_step(zc_, yb_);
-        rotate(t0 + tt);
+        if constexpr (RL2) {
+          if ((t0 + tt + 1) % TC == 0) rot_t = t0 + tt;
+        } else {
+          rotate(t0 + tt);
+        }
       };
       bool have_next = false;
       if constexpr (PIPE) {
