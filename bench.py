@@ -349,13 +349,12 @@ def pmc_traffic(kernel_substr: str, evals: int):
     return None, None
 
 
-# the instantiation each configuration runs: fixedz_loglik_kernel<NP, M, LEAD, RECORD, STEADY, SPLIT_FORM, PIPE>
+# the instantiation each configuration runs: fixedz_loglik_kernel<NP, M, LEAD, RECORD, STEADY, SPLIT_FORM>
 # (DNS: frozen-covariance steady state by default; GNS5: full recursion unless YFM_GNS5_STEADY=1)
-DOMINANT = {(KIND_DNS, "steady"): "fixedz_loglik_kernel<30, 3, 1, false, true, false, false>",
-            (KIND_DNS, "pipe"): "fixedz_loglik_kernel<30, 3, 1, false, true, false, true>",
-            (KIND_DNS, "full"): "fixedz_loglik_kernel<30, 3, 1, false, false, false, false>",
-            (KIND_GNS, "steady"): "fixedz_loglik_kernel<30, 5, 2, false, true, false, false>",
-            (KIND_GNS, "full"): "fixedz_loglik_kernel<30, 5, 2, false, false, false, false>",
+DOMINANT = {(KIND_DNS, "steady"): "fixedz_loglik_kernel<30, 3, 1, false, true, false>",
+            (KIND_DNS, "full"): "fixedz_loglik_kernel<30, 3, 1, false, false, false>",
+            (KIND_GNS, "steady"): "fixedz_loglik_kernel<30, 5, 2, false, true, false>",
+            (KIND_GNS, "full"): "fixedz_loglik_kernel<30, 5, 2, false, false, false>",
             (KIND_TVL, "fp64"): "tvl_loglik_kernel", (KIND_TVL, "certified"): "tvl_dd_loglik_kernel"}
 
 
@@ -367,7 +366,7 @@ def dominant_kernel(kind, prec):
         return DOMINANT[(kind, "full")]
     if kind == KIND_GNS:
         return DOMINANT[(kind, "steady" if env("YFM_GNS5_STEADY", "0").startswith("1") else "full")]
-    return DOMINANT[(kind, "pipe" if env("YFM_DNS_PIPE", "0").startswith("1") else "steady")]
+    return DOMINANT[(kind, "steady")]
 
 
 def roofline(kind, prec, N, M, T, T_use, B, P, kernel_ms, steady_lane_steps=0):

@@ -176,6 +176,30 @@ def test_speculation_is_bitwise_neutral(engine, panel):
         assert a["n_evals"] == b["n_evals"]
 
 
+@pytest.mark.parametrize("switch", [{"YFM_EST_GROUPS": "1"}, {"YFM_EST_GROUPS": "3"}, {"YFM_EST_ZEROCOPY": "0"},
+                                    {"YFM_EST_THREADS": "1"}, {"YFM_EST_STATS": "1"}])
+def test_estimator_tuning_switches_are_bitwise_neutral(engine, panel, switch):
+    """The estimator's tuning switches (csrc/yfm_estimate.hip: chain groups on their own streams, zero-copy
+    page-locked rounds, host threads, the per-phase statistics print) change how a round is scheduled, never
+    what a chain computes: 40 windows (two chain groups by default) give the same chains bit for bit and the
+    same evaluation count as the defaults."""
+    import os
+    Y, mats = panel
+    engine.set_panel(Y, mats)
+    starts = S.theta_batch(KIND_DNS, 40, seed=73, bad_frac=0.1, scale=0.08)
+    win = (80 - np.arange(40) % 30).astype(np.int32)
+    a = engine.estimate(KIND_DNS, starts, space=0, T_use=win, iterations=60, max_group_iters=2)
+    os.environ.update(switch)
+    try:
+        b = engine.estimate(KIND_DNS, starts, space=0, T_use=win, iterations=60, max_group_iters=2)
+    finally:
+        for k in switch:
+            os.environ.pop(k, None)
+    for k in ("theta_c", "p", "init_c", "ll", "status"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=f"{k} with {switch}")
+    assert a["n_evals"] == b["n_evals"] > 0
+
+
 @pytest.mark.parametrize("kind_name", ["GNS5", "TVL"])
 def test_speculation_tree_other_models(engine, panel, kind_name):
     """The speculation tree on the larger simplices (GNS5: 48 parameters, TVλ: 31, certified

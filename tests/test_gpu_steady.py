@@ -75,30 +75,6 @@ def test_steady_is_batch_independent(engine, config2):
     np.testing.assert_array_equal(a[3::7], c)
 
 
-def test_pipelined_steady_blocks_are_bitwise_the_default(engine, config2):
-    """YFM_DNS_PIPE=1 (opt-in since round 4: FP64 MFMA and VALU share one pipe on gfx950) issues the next
-    block's Z'ỹ MFMAs inside a steady block; the same arithmetic per step, so the same bits — also with a
-    NaN column after the freeze and ragged windows."""
-    Y, mats, Th = config2
-    Y = Y.copy(order="F")
-    Y[:, [300, 301]] = np.nan
-    engine.set_panel(Y, mats)
-    sub = np.asfortranarray(Th[:, :4096 + 40])
-    tu = np.full(sub.shape[1], Y.shape[1], dtype=np.int32)
-    tu[-1] = 250
-    tu[100:110] = 450
-    base = engine.loglik(KIND_DNS, sub, T_use=tu)
-    st = engine.last_steady()
-    os.environ["YFM_DNS_PIPE"] = "1"
-    try:
-        piped = engine.loglik(KIND_DNS, sub, T_use=tu)
-        st_p = engine.last_steady()
-    finally:
-        os.environ.pop("YFM_DNS_PIPE", None)
-    assert st > 0 and st_p == st
-    np.testing.assert_array_equal(piped, base)
-
-
 def test_steady_parity_config2_sample(engine, config2):
     Y, mats, Th = config2
     engine.set_panel(Y, mats)

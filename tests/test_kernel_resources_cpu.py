@@ -16,11 +16,11 @@ READELF = Path("/opt/rocm/lib/llvm/bin/llvm-readelf")
 # kernel (demangled-name fragment of the mangled symbol) → max scratch bytes per lane
 BUDGETS = {
     # config 2 / 4: DNS, NP = 30, loglik mode with the frozen-covariance steady state
-    "fixedz_loglik_kernelILi30ELi3ELi1ELb0ELb1ELb0ELb0E": 0,
+    "fixedz_loglik_kernelILi30ELi3ELi1ELb0ELb1ELb0EE": 0,
     # the same with the full recursion (YFM_DNS_STEADY=0, the steady-vs-full gate)
-    "fixedz_loglik_kernelILi30ELi3ELi1ELb0ELb0ELb0ELb0E": 0,
+    "fixedz_loglik_kernelILi30ELi3ELi1ELb0ELb0ELb0EE": 0,
     # config 5: GNS5, NP = 30, full recursion
-    "fixedz_loglik_kernelILi30ELi5ELi2ELb0ELb0ELb0ELb0E": 0,
+    "fixedz_loglik_kernelILi30ELi5ELi2ELb0ELb0ELb0EE": 0,
     # config 3: certified TVλ at L = 4
     "tvl_dd_loglik_kernelILi4ELb0E": 0,
 }

@@ -79,15 +79,16 @@ def build(force: bool = False, verbose: bool = True) -> Path:
               + [Path(__file__).stat().st_mtime])
     todo = [(s, o) for s, o in zip(srcs, objs)
             if force or not o.exists() or o.stat().st_mtime < max(s.stat().st_mtime, hdr)]
-    if todo:
-        STAMP.unlink(missing_ok=True)  # a half-finished rebuild must not pass as the stamped one
+    # a half-finished rebuild (a failed compile or link) must not pass as the stamped one: the stamp goes now and
+    # is written back only after the link succeeded, so the library beside it was made with these flags
+    STAMP.unlink(missing_ok=True)
     with ThreadPoolExecutor(max_workers=max(1, min(len(todo), 4))) as ex:
         list(ex.map(cc, todo))
-    STAMP.write_text(_stamp())
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(LIB)]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
+    STAMP.write_text(_stamp())
     return LIB
 
 

@@ -216,7 +216,7 @@ __device__ __forceinline__ bool init_state(const Params<M, LEAD>& p, double (&be
 template <int M, bool SYM = false>
 struct Capacitance {
   __device__ __forceinline__ static void solve(const double (&P)[M][M], const double (&G)[M][M], double sigma2,
-                                               double (&W)[M][M], double& det, bool* swapped = nullptr) {
+                                               double (&W)[M][M], double& det) {
     double A[M][M];
     double X[M][M];
 #pragma unroll
@@ -244,7 +244,6 @@ struct Capacitance {
         p = gt ? i : p;
       }
       sgn = (p != k) ? -sgn : sgn;
-      if (swapped) *swapped = *swapped || (p != k);  // (timing/statistics probes only)
 #pragma unroll
       for (int i = k + 1; i < M; ++i) {
         const bool s = (p == i);

@@ -515,11 +515,6 @@ struct FixedZFilter {
       last_det = det;
       last_q = q;
       sumq += q;
-#ifdef YFM_DEBUG_LANE
-      if (blockIdx.x == 0 && threadIdx.x < YFM_DEBUG_LANE)
-        printf("dbg L%d t %d fast det %.17g q %.17g P00 %.17g P44 %.17g b0 %.17g z0 %.17g\n", (int)threadIdx.x, t, det, q, Pm[0][0],
-               Pm[M - 1][M - 1], beta[0], zc[0]);
-#endif
       return;
     }
     const bool act = t < my_steps;
@@ -543,10 +538,6 @@ struct FixedZFilter {
         sumq += last_q;
         neg = neg || (last_det < 0.0);
       }
-#ifdef YFM_DEBUG_LANE
-      if (blockIdx.x == 0 && threadIdx.x < YFM_DEBUG_LANE)
-        printf("dbg L%d t %d pred P00 %.17g P44 %.17g b0 %.17g\n", (int)threadIdx.x, t, Pm[0][0], Pm[M - 1][M - 1], beta[0]);
-#endif
       return;
     }
     double det, q;
@@ -576,11 +567,6 @@ struct FixedZFilter {
       }
       sumq += last_q;
     }
-#ifdef YFM_DEBUG_LANE  // diagnostic builds only (tools/dbg_variants.sh)
-    if (blockIdx.x == 0 && threadIdx.x < YFM_DEBUG_LANE)
-      printf("dbg L%d t %d data det %.17g q %.17g P00 %.17g P44 %.17g b0 %.17g z0 %.17g yb %.17g %.17g\n", (int)threadIdx.x, t, det, q,
-             Pm[0][0], Pm[M - 1][M - 1], beta[0], zc[0], yb_c.x, yb_c.y);
-#endif
   }
 
   // the state after step t into slot t − max(0, my_steps − rec_len) (the last rec_len steps)

@@ -109,10 +109,13 @@ __device__ __forceinline__ void fd_propagate(const double* par, const dd (&b)[M]
 // decode θ_b in dd (transform_params + set_params!) and run initialize_filter (filter.jl:1-10) into the
 // record r of one deferred candidate.  Called by one lane of the candidate's group inside
 // fixedz_dd_loglik_kernel (round 4: a separate init kernel cost a ~4.4 µs launch on every config-2 call,
-// deferred lanes or not); not inlined, so its ~6×6 / 15×15 dd solves do not shape the filter's registers.
+// deferred lanes or not).  DNS inlines it (its 6×6 solve fits beside the filter's registers; a call would make
+// the kernel save callee registers to scratch, and a kernel with a private segment costs its dispatch even when
+// the deferral list is empty); GNS5 calls it out of line (fd_init_record_call) so that its 15×15 dd solve does
+// not shape the filter's registers.
 template <int M, int LEAD>
-__device__ __noinline__ void fd_init_record(const double* __restrict__ theta, int P, int space, int b,
-                                            double* __restrict__ r) {
+__device__ __forceinline__ void fd_init_record(const double* __restrict__ theta, int P, int space, int b,
+                                               double* __restrict__ r) {
   using R = FdRec<M>;
   {
   const double* th = theta + (size_t)b * P + LEAD;
@@ -209,6 +212,12 @@ __device__ __noinline__ void fd_init_record(const double* __restrict__ theta, in
   }
 }
 
+template <int M, int LEAD>
+__device__ __noinline__ void fd_init_record_call(const double* __restrict__ theta, int P, int space, int b,
+                                                 double* __restrict__ r) {
+  fd_init_record<M, LEAD>(theta, P, space, b, r);
+}
+
 template <int L, int M, int LEAD, bool RECORD>
 __global__ __launch_bounds__(kFdBlock) void fixedz_dd_loglik_kernel(
     double* __restrict__ rec, const int* __restrict__ defer_list, const int* __restrict__ defer_count,
@@ -243,7 +252,12 @@ __global__ __launch_bounds__(kFdBlock) void fixedz_dd_loglik_kernel(
   const int nobs = T_use ? T_use[b] : T;
 
   if (tid == 0) s_nobs_max = 0;
-  if (live && j == 0) fd_init_record<M, LEAD>(theta, P, space, b, rec + (size_t)gg * R::Len);
+  if (live && j == 0) {
+    if constexpr (M == 3)
+      fd_init_record<M, LEAD>(theta, P, space, b, rec + (size_t)gg * R::Len);
+    else
+      fd_init_record_call<M, LEAD>(theta, P, space, b, rec + (size_t)gg * R::Len);
+  }
   __syncthreads();  // the record (global memory, this workgroup) before its lanes read it
   const double* r = rec + (size_t)gg * R::Len;
   double* par = s_par + grp * R::Par;

@@ -33,42 +33,15 @@
 namespace yfm {
 
 constexpr int kBlock = 256;  // 4 waves: one per SIMD of a CU
-constexpr int kTC = 64;  // panel columns per LDS chunk (DNS; GNS5 and the pipelined DNS blocks keep 32 for LDS)
-// Look-ahead MFMA blocks (DNS steady state, round 5): a steady block issues the NEXT block's 64 Z'ỹ MFMAs before
-// its own 16 mean updates and stores their results after them, into the other of two scratch buffers — the
-// accumulator read-out, the LDS writes and their landing no longer sit between a block's MFMAs and its first step
-// (the store tail, ≈ 1,100 cycles per block).  FP64 MFMA and FP64 VALU share the pipe, so the order costs no
-// arithmetic; the price is the second buffer (32-column panel chunks) and 64 AGPRs live across the steady steps.
-#ifndef YFM_DNS_SIGMA  // 0: the 16×16×4 D tiles stored as four 8-byte LDS writes per tile (rounds 1–4)
-#define YFM_DNS_SIGMA 1
-#endif
-#ifndef YFM_EARLY_CHUNKS  // 0: the first two panel chunks loaded after the setup, one round trip each (round 4)
-#define YFM_EARLY_CHUNKS 1
-#endif
-#ifndef YFM_MIDBLOCK_STEADY  // 0: a block that starts with the full recursion runs it to the block's end (round 4)
-#define YFM_MIDBLOCK_STEADY 1
-#endif
-#ifndef YFM_AF_IN_AGPR
-#define YFM_AF_IN_AGPR 1
-#endif
-#ifndef YFM_AF_AGPR_GNS
-#define YFM_AF_AGPR_GNS 1
-#endif
-#ifndef YFM_STORE_INTERLEAVE
-#define YFM_STORE_INTERLEAVE 2  // 1: two tile groups (4, 4); 2: three (4, 2, 2), the default; 0: stores after each group
-#endif
-#ifndef YFM_ROTATE_LATE  // a steady block's chunk rotation at the next block's start (0: after its steps, round 4)
-#define YFM_ROTATE_LATE 2  // 1: only a whole steady block's; 2: every block-end rotation (default)
-#endif
-#ifndef YFM_DNS_LOOKAHEAD
-#define YFM_DNS_LOOKAHEAD 0
-#endif
+constexpr int kTC = 64;  // panel columns per LDS chunk (DNS; GNS5 keeps 32: its z̃ scratch takes the LDS)
+// Variants measured and not kept live in git history and DESIGN.md §3.1 / §6 (round 5 pruned them from the
+// library): the look-ahead and pipelined steady blocks (the next block's MFMAs among the mean updates — FP64
+// MFMA and VALU share one pipe on gfx950: 4.5% and 1.5% slower), four 8-byte z̃ stores per tile instead of
+// the σ-permuted 16-byte ones, the first chunks loaded after the setup, no mid-block steady switch, MFMA A
+// operands copied to VGPRs, two (4, 4) tile groups, chunk rotations after a block's steps, and the timing
+// probes (phase cycle counters, MFMAs issued twice, z̃ never stored) that located the costs.
 constexpr bool kMfma4 = true;   // GNS5 Z'ỹ on v_mfma_f64_4x4x4_4b_f64 (DNS keeps v_mfma_f64_16x16x4_f64)
 constexpr bool kZBasis = true;  // GNS5 fragments e = 1 − e^{−λm} against (ỹ, ỹ/m): see the kernel
-#ifndef YFM_PIPE_VALU
-#define YFM_PIPE_VALU 8
-#endif
-constexpr int kPipeValu = YFM_PIPE_VALU;  // VALU instructions between two MFMAs of a pipelined steady step
 
 __global__ void prep_panel_kernel(const double* __restrict__ Y, int N, int T, int np, int ldp,
                                   double* __restrict__ out) {
@@ -165,7 +138,7 @@ typedef double yfm_double4 __attribute__((ext_vector_type(4)));
 // computed one step ahead, inside the same basic block as the update.
 // A wave-uniform fast path (no NaN column, every lane active, every lane collapsed,
 // t ≥ 1) carries no per-lane masking; everything else takes the general path.
-template <int NP, int M, int LEAD, bool RECORD, bool STEADY_ = false, bool SPLIT_FORM = false, bool PIPE_ = false>
+template <int NP, int M, int LEAD, bool RECORD, bool STEADY_ = false, bool SPLIT_FORM = false>
 __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     const double* __restrict__ theta, int P, int B, int space, const double* __restrict__ panel, int T, int N,
     const double* __restrict__ mats, const int* __restrict__ T_use, double* __restrict__ out,
@@ -175,9 +148,8 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   constexpr int LDP = NP + 4;
   // panel columns per LDS chunk: 64 for DNS (a chunk rotation, with its two block barriers, every 64 steps
   // instead of 32: 0.2040 → 0.2022 ms at config 2, profiles/r4/ab23/); 32 where the LDS is taken by GNS5's
-  // z̃ scratch or the pipelined block's second buffer
-  constexpr bool LA_ = YFM_DNS_LOOKAHEAD && STEADY_ && !RECORD && M == 3 && !PIPE_ && (NP <= 32);
-  constexpr int TC = (M == 3 && !PIPE_ && !LA_) ? kTC : 32;
+  // z̃ scratch
+  constexpr int TC = (M == 3) ? kTC : 32;
   constexpr bool USE_MFMA_ = (M - 1 == 2 || M - 1 == 4) && (NP <= 32);
   // frozen-covariance steady state (FixedZFilter): the loglik-mode DNS instantiation
   // with STEADY_ (the plain instantiation is the full recursion, YFM_DNS_STEADY=0)
@@ -205,23 +177,14 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   constexpr int SS = 64 * NZ + 2;             // scratch row stride (doubles): one row per step
   // (also the fragment staging image of 32 candidates: 32·RPC rows of 4·NK + 1 maturities)
   constexpr int SCR = USE_MFMA ? ((TB * SS > 32 * RPC * (4 * NK + 1)) ? TB * SS : 32 * RPC * (4 * NK + 1)) : 2;
-  // PIPE (DNS steady state): a steady block issues the NEXT block's Z'ỹ MFMAs between its own mean
-  // updates — the matrix pipe and the VALU then work side by side instead of one after the other — into
-  // a second scratch buffer per wave (2 × 16.6 KB per wave: 151.5 KB of LDS at NP = 32)
-  constexpr bool PIPE = PIPE_ && STEADY && NZ == 2 && !ZB;
-  constexpr bool LA = LA_ && STEADY && NZ == 2 && !ZB;
-  constexpr int NBUF = (PIPE || LA) ? 2 : 1;
   static_assert(NZ == 2 * LEAD, "loading columns come in (S, C) pairs per gamma");
   static_assert(NP % 2 == 0, "double2 panel reads");
   static_assert(TC % TB == 0, "MFMA blocks tile the panel chunk");
   __shared__ __attribute__((aligned(16))) double sh[2][CH];
-  __shared__ __attribute__((aligned(16))) double scratch[kBlock / 64][NBUF][SCR];
+  __shared__ __attribute__((aligned(16))) double scratch[kBlock / 64][SCR];
   __shared__ int s_nobs_max;
   __shared__ double s_rm[ZB ? NP : 1];  // 1/m_i (0 past N)
 
-#ifdef YFM_PHASE_PROBE  // timing probe builds only (tools/phase_run.py): per-wave cycles by phase, printf'd
-  const long long ph_entry = __builtin_readcyclecounter();
-#endif
   if (flags_next && blockIdx.x == 0 && threadIdx.x < kFlagsPerBank) flags_next[threadIdx.x] = 0u;  // the next launch's counters
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -251,11 +214,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   };
   // EARLY: chunks 0 and 1 issued before the setup, so their HBM latency hides under the θ decode and the
   // loadings instead of two serial round trips after it (stored to LDS where the staging starts below)
-  constexpr bool MID = YFM_MIDBLOCK_STEADY != 0;
-  constexpr bool RL = YFM_ROTATE_LATE != 0;
-  constexpr bool RL2 = YFM_ROTATE_LATE == 2;  // every path's block-end rotation deferred (full steps too)
-  constexpr bool AF_AGPR_GNS = YFM_AF_AGPR_GNS && M == 5;
-  constexpr bool EARLY = YFM_EARLY_CHUNKS != 0 && M == 3 && NP <= 32;  // GNS5 and NP > 32 spill with the 2·PER registers
+  constexpr bool EARLY = M == 3 && NP <= 32;  // GNS5 and NP > 32 spill with the 2·PER registers
   double pre0[EARLY ? PER : 1], pre1[EARLY ? PER : 1];
   if constexpr (EARLY) {
     load_into(pre0, 0);
@@ -285,7 +244,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
       const int w0 = min(blockIdx.x * kBlock + wave * 64, B - 1);  // first row of this wave's range
       const int n = min(64, B - w0) * kP;
       const double* src = theta + (size_t)w0 * kP;
-      double* thl = scratch[wave][0];
+      double* thl = scratch[wave];
       double v[kP];
 #pragma unroll
       for (int r = 0; r < kP; ++r) {
@@ -303,10 +262,6 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
   decode_params<M, LEAD>(th_row, space, p);
   __builtin_amdgcn_s_waitcnt(0xc07f);  // the rows are read before the fragment staging reuses the scratch
   __builtin_amdgcn_wave_barrier();
-#ifdef YFM_PHASE_PROBE
-  asm volatile("" ::"v"(p.sigma2));
-  const long long ph_s1 = __builtin_readcyclecounter();
-#endif
 
   double Zc[NZ][NP];
 #pragma unroll
@@ -342,20 +297,17 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     }
   }
 
-#ifdef YFM_PHASE_PROBE
-  asm volatile("" ::"v"(G[1][2]));
-  const long long ph_s2 = __builtin_readcyclecounter();
-#endif
   // MFMA A fragments: tile r, k-step kk — lane l holds Z of pair p = 16r + σ(l & 15)
   // (candidate p / NZ of this wave, column p % NZ) at maturity 4kk + (l >> 4).
   // Gathered once through the wave's scratch, 16 candidates at a time.
   // σ (the 16×16×4 form only): row i = g + 4q of a tile holds pair 16r + 4g + q, so the four D values a lane
   // holds (rows g, g+4, g+8, g+12 of one step) are four consecutive pairs — two 16-byte LDS stores per tile
   // instead of four 8-byte ones, and still one candidate's z̃ in consecutive doubles for the step reads
-  constexpr bool SIGMA = YFM_DNS_SIGMA && USE_MFMA && !ZB && !(kMfma4 && NZ == 4);
-  // IL: the first row-tile group's stores interleaved with the second group's MFMAs (NP 29–32: one per k-step)
-  constexpr bool IL = YFM_STORE_INTERLEAVE && SIGMA && NRT == 2 * RGN && NK == 2 * RGN;
-  constexpr bool IL5 = YFM_STORE_INTERLEAVE && ZB && NK == NRTA;  // GNS5: the same across step pairs
+  constexpr bool SIGMA = USE_MFMA && !ZB && !(kMfma4 && NZ == 4);
+  // IL: the row tiles in three groups (4, 2, 2), each group's stores interleaved with the next group's MFMAs
+  // (NP 29–32: one store per k-step)
+  constexpr bool IL = SIGMA && NRT == 2 * RGN && NK == 2 * RGN;
+  constexpr bool IL5 = ZB && NK == NRTA;  // GNS5: the same across step pairs
   auto sigma = [](int i) { return SIGMA ? 4 * (i & 3) + (i >> 2) : i; };
   double Af[USE_MFMA ? NRTA : 1][USE_MFMA ? NK : 1];
   double rlam[LEAD];  // 1/λ_l (z-basis fragments)
@@ -367,7 +319,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     static_assert(32 * RPC * ZS <= SCR, "staging fits the scratch");
     // two rounds of 32 candidates (round 3: four of 16, with a block barrier after each write and read — the
     // scratch is the wave's own, so the wave's LDS counter and a wave barrier order it; profiles/r4/ab13)
-    double* st = scratch[wave][0];
+    double* st = scratch[wave];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       if ((lane >> 5) == h) {
@@ -402,9 +354,6 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     }
   }
 
-#ifdef YFM_PHASE_PROBE
-  const long long ph_s3 = __builtin_readcyclecounter();
-#endif
   FixedZFilter<M, LEAD, RECORD, STEADY, SPLIT_FORM> f;
   f.p = p;
   f.steady_ok = steady != 0;
@@ -423,10 +372,6 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
       }
     f.init_ok = init_rec[(size_t)q * B + bb] != 0.0;
   }
-#ifdef YFM_PHASE_PROBE
-  asm volatile("" ::"v"(f.Pm[0][1]), "v"(f.R[0][1]));
-  const long long ph_s4 = __builtin_readcyclecounter();
-#endif
   // ill-conditioned Z'Z: this candidate is evaluated by the double-double capacitance kernel
   // instead (yfm_fixedz_dd.hip); its lane here runs along without writing
   const bool defer = live && !f.collapsed;
@@ -492,30 +437,21 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     }
   };
 
-#ifdef YFM_PHASE_PROBE
-  long long ph_t0 = __builtin_readcyclecounter(), ph_bound = 0, ph_bload = 0, ph_mfma = 0, ph_dec = 0, ph_st = 0, ph_full = 0;
-  int ph_nst = 0, ph_nfull = 0;
-#endif
   if constexpr (USE_MFMA) {
     unsigned int steady_steps = 0;  // STEADY: this wave's steady steps (one atomic at the end: a per-block
                                     // atomic would put its latency on the next global load's wait)
-    int buf = 0;          // PIPE: this block's scratch buffer
-    bool have_z = false;  // PIPE: this block's z̃ were formed during the previous (steady) block
-    int rot_t = -1;  // RL: a whole steady block's chunk rotation, deferred to the next block's start
+    // a block-end chunk rotation, deferred to the next block's start: with its barrier after the steps the
+    // compiler sinks the steps' arithmetic below it and issues all 32 operand reads up front (128 registers)
+    int rot_t = -1;
     for (int t0 = 0; t0 < nsteps; t0 += TB) {
-      if constexpr (RL) {
-        if (rot_t >= 0) {
-          rotate(rot_t);
-          rot_t = -1;
-        }
+      if (rot_t >= 0) {
+        rotate(rot_t);
+        rot_t = -1;
       }
       // the freeze rule's contraction bound, once per lane, at a block boundary before the block's MFMA
       // accumulators are live (FixedZFilter::prepare_bound)
-#ifdef YFM_PHASE_PROBE
-      const long long ph_a = __builtin_readcyclecounter();
-#endif
       if constexpr (STEADY) f.prepare_bound();
-      if constexpr (YFM_AF_IN_AGPR && (SIGMA || AF_AGPR_GNS)) {
+      if constexpr (SIGMA || M == 5) {
         // the A fragments stay in AGPRs, where the 16×16×4 MFMA reads them as its A operand (left to itself the
         // allocator copies each one to a VGPR before its MFMA: 128 v_accvgpr_read per block)
 #pragma unroll
@@ -523,18 +459,13 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
 #pragma unroll
           for (int kk = 0; kk < NK; ++kk) asm volatile("" : "+a"(Af[r][kk]));
       }
-#ifdef YFM_PHASE_PROBE
-      long long ph_a2 = __builtin_readcyclecounter(), ph_a3 = ph_a2;
-#endif
-      double* scr = scratch[wave][(PIPE || LA) ? buf : 0];
+      double* scr = scratch[wave];
       // ---- z̃ for steps t0 .. t0+15 of all 64 candidates: NRT·NK MFMAs ----
       const double* cb = col_of(t0);  // TB consecutive columns of one chunk
       // the block's NaN flags, one column per lane, read before the MFMAs so the steady-block vote after them
       // does not wait for an LDS round trip (0.2179 → 0.2168 ms at config 2, profiles/r4/ab9/)
       const double col_flag = cb[min(lane, TB - 1) * LDP + NP + 2];
-      if (have_z) {
-        // (PIPE) already in scratch[wave][buf]
-      } else if constexpr (ZB && IL5) {
+      if constexpr (ZB && IL5) {
         // as below, software-pipelined over the step pairs: step pair sp − 1's 8 results are stored one per
         // k-step of step pair sp's MFMAs (the wave issues the stores while the matrix pipe works)
         double accp[NRTA];
@@ -648,11 +579,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
           const int m = 4 * kk + (lane >> 4);
           bvk[kk] = (m < NP) ? cb[(lane & 15) * LDP + m] : 0.0;  // B[k = m][col = step]
         }
-#ifdef YFM_PHASE_PROBE
-        __builtin_amdgcn_s_waitcnt(0xc07f);
-        ph_a3 = __builtin_readcyclecounter();
-#endif
-        if constexpr (IL && YFM_STORE_INTERLEAVE == 2) {
+        if constexpr (IL) {
           // three groups of 4, 2, 2 tiles: the first group's 8 stores during the second group's MFMAs, the
           // second's 4 during the third's, so only the last 2 tiles' 4 stores trail the block
           constexpr int H = RGN / 2;
@@ -699,34 +626,6 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
           }
 #pragma unroll
           for (int r = 0; r < H; ++r) store_tile(scr, RGN + H + r, a3[r]);
-        } else if constexpr (IL) {
-          // the first group's 8 16-byte stores issued one per k-step of the second group's MFMAs (the wave
-          // issues them while the matrix pipe works) instead of back to back between the groups
-          yfm_double4 a1[RGN], a2[RGN];
-#pragma unroll
-          for (int r = 0; r < RGN; ++r) a1[r] = a2[r] = yfm_double4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-          for (int kk = 0; kk < NK; ++kk)
-#pragma unroll
-            for (int r = 0; r < RGN; ++r)
-              a1[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(Af[r][kk], bvk[kk], a1[r], 0, 0, 0);
-#pragma unroll
-          for (int kk = 0; kk < NK; ++kk) {
-#pragma unroll
-            for (int r = 0; r < RGN; ++r)
-              a2[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(Af[RGN + r][kk], bvk[kk], a2[r], 0, 0, 0);
-            const int r1 = kk >> 1, h = kk & 1;
-            double* d = scr + (lane & 15) * SS + 16 * r1 + 4 * (lane >> 4) + 2 * h;
-            *reinterpret_cast<double2*>(d) = make_double2(a1[r1][2 * h], a1[r1][2 * h + 1]);
-          }
-          __builtin_amdgcn_sched_group_barrier(0x008, RGN * NK, 0);  // the first group's MFMAs
-#pragma unroll
-          for (int kk = 0; kk < NK; ++kk) {
-            __builtin_amdgcn_sched_group_barrier(0x008, RGN, 0);  // a k-step of the second group
-            __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);    // one store of the first
-          }
-#pragma unroll
-          for (int r = 0; r < RGN; ++r) store_tile(scr, RGN + r, a2[r]);
         } else {
 #pragma unroll
         for (int r0 = 0; r0 < NRT; r0 += RGN) {
@@ -739,42 +638,13 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
             for (int r = 0; r < RGN; ++r)
               acc[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(Af[r0 + r][kk], bvk[kk], acc[r], 0, 0, 0);
           // D[row][col = step]: lane l holds step l & 15, rows (l >> 4) + 4q = pairs 16r + 4(l >> 4) + q
-#ifdef YFM_PROBE_NOWRITE  // timing probe: results kept in registers, never stored (the block reads stale z̃)
-#pragma unroll
-          for (int r = 0; r < RGN; ++r) asm volatile("" ::"a"(acc[r]));
-#else
 #pragma unroll
           for (int r = 0; r < RGN; ++r) store_tile(scr, r0 + r, acc[r]);
-#endif
         }
         }
-#ifdef YFM_PROBE_MFMA2X  // timing probe: the block's MFMAs a second time, results discarded
-        double bvq[NK];  // opaque copies: the second pass must not be merged with the first
-#pragma unroll
-        for (int kk = 0; kk < NK; ++kk) {
-          bvq[kk] = bvk[kk];
-          asm volatile("" : "+v"(bvq[kk]));
-        }
-#pragma unroll
-        for (int r0 = 0; r0 < NRT; r0 += RGN) {
-          yfm_double4 acc[RGN];
-#pragma unroll
-          for (int r = 0; r < RGN; ++r) acc[r] = yfm_double4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-          for (int kk = 0; kk < NK; ++kk)
-#pragma unroll
-            for (int r = 0; r < RGN; ++r)
-              acc[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(Af[r0 + r][kk], bvq[kk], acc[r], 0, 0, 0);
-#pragma unroll
-          for (int r = 0; r < RGN; ++r) asm volatile("" ::"a"(acc[r]));
-        }
-#endif
       }
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's scratch writes landed
       __builtin_amdgcn_wave_barrier();
-#ifdef YFM_PHASE_PROBE
-      const long long ph_b = __builtin_readcyclecounter();
-#endif
       const int tend = min(TB, nsteps - t0);
       // a block of steady steps: every lane of the wave frozen, and every step of the block a data
       // step of every lane (no NaN column, t ≥ 1, inside every lane's window)
@@ -787,36 +657,6 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
           // (0.236 → 0.217 ms at config 2, profiles/r3/probes/dns_steady_nan/)
           const bool col_nan = (lane < tend) && (col_flag != 0.0);
           blk_steady = !__any(col_nan);
-        }
-      }
-#ifdef YFM_PHASE_PROBE
-      const long long ph_c = __builtin_readcyclecounter();
-#endif
-      // LA: the next block's Z'ỹ MFMAs, issued now, stored after this block's steady steps (into the other buffer)
-      bool la_next = false;
-      yfm_double4 la_acc[LA ? NRT : 1];
-      if constexpr (LA) {
-        if (blk_steady && tend == TB && t0 + TB < nsteps) {
-          la_next = true;
-          const double* nb = col_of(t0 + TB);  // resident: the next 16 columns are in this or the next chunk
-          double bvn[NK];
-#pragma unroll
-          for (int kk = 0; kk < NK; ++kk) {
-            const int m = 4 * kk + (lane >> 4);
-            bvn[kk] = (m < NP) ? nb[(lane & 15) * LDP + m] : 0.0;
-          }
-#pragma unroll
-          for (int r = 0; r < NRT; ++r) la_acc[r] = yfm_double4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-          for (int kk = 0; kk < NK; ++kk)
-#pragma unroll
-            for (int r = 0; r < NRT; ++r)
-              la_acc[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(Af[r][kk], bvn[kk], la_acc[r], 0, 0, 0);
-          // the first half of the tiles now (their MFMAs finished while the second half issued); the second
-          // half after the steps, so only 32 accumulator registers stay live across them
-          double* scn = scratch[wave][buf ^ 1];
-#pragma unroll
-          for (int r = 0; r < NRT / 2; ++r) store_tile(scn, r, la_acc[r]);
         }
       }
       // step operands for tt are read one step ahead (hides the LDS latency at 1 wave/SIMD)
@@ -850,11 +690,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
         metan_ = *reinterpret_cast<const double2*>(cb + tn * LDP + NP + 2);
         do_step(t, zc_, yb_, meta_);
         record(t);
-        if constexpr (RL2) {
-          if ((t + 1) % TC == 0) rot_t = t;  // (RL2) deferred to the next block's start, as a steady block's
-        } else {
-          rotate(t);
-        }
+        if ((t + 1) % TC == 0) rot_t = t;  // the chunk rotation, deferred to the next block's start
       };
       // the mean update only, with the cached factors of S (bitwise the full step's values for a frozen lane);
       // operands read one step ahead as in `half`
@@ -863,77 +699,10 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
         read_z(tn, zn_);
         ybn_ = *reinterpret_cast<const double2*>(cb + tn * LDP + NP);
         f.steady_step(zc_, yb_);
-        if constexpr (RL2) {
-          if ((t0 + tt + 1) % TC == 0) rot_t = t0 + tt;
-        } else {
-          rotate(t0 + tt);
-        }
+        if ((t0 + tt + 1) % TC == 0) rot_t = t0 + tt;
       };
-      bool have_next = false;
-      if constexpr (PIPE) {
-        if (blk_steady && tend == TB && t0 + TB < nsteps) {
-          // the steady block unrolled, with the next block's Z'ỹ MFMAs spread over its steps: unit u of
-          // the 4·NK units (row-tile pair u / NK, k-step u % NK; two MFMAs each, one per tile of the pair)
-          // runs in step u·TB / (4·NK); a pair's accumulators go to the other scratch buffer after its last
-          // k-step (the D layout of the block form above)
-          constexpr int U = (NRT / 2) * NK;
-          double* scn = scratch[wave][buf ^ 1];
-          const double* nb = col_of(t0 + TB);  // resident: chunk (t0+16)/32 is in LDS while chunk t0/32 runs
-          double zq[2][NZ];
-          double2 ybq[2];
-#pragma unroll
-          for (int j = 0; j < NZ; ++j) zq[0][j] = zc[j];
-          ybq[0] = yb;
-          yfm_double4 pa0 = yfm_double4{0.0, 0.0, 0.0, 0.0}, pa1 = pa0;
-#pragma unroll
-          for (int tt = 0; tt < TB; ++tt) {
-            const int cur = tt & 1, nx = cur ^ 1;
-            const int tn = min(tt + 1, TB - 1);
-            read_z(tn, zq[nx]);
-            ybq[nx] = *reinterpret_cast<const double2*>(cb + tn * LDP + NP);
-#pragma unroll
-            for (int u = (tt * U) / TB; u < ((tt + 1) * U) / TB; ++u) {
-              const int rp = 2 * (u / NK), kk = u % NK;
-              if (kk == 0) {
-                pa0 = yfm_double4{0.0, 0.0, 0.0, 0.0};
-                pa1 = pa0;
-              }
-              const int m = 4 * kk + (lane >> 4);
-              const double bv = (m < NP) ? nb[(lane & 15) * LDP + m] : 0.0;
-              pa0 = __builtin_amdgcn_mfma_f64_16x16x4f64(Af[rp][kk], bv, pa0, 0, 0, 0);
-              pa1 = __builtin_amdgcn_mfma_f64_16x16x4f64(Af[rp + 1][kk], bv, pa1, 0, 0, 0);
-              if (kk == NK - 1) {
-                store_tile(scn, rp, pa0);
-                store_tile(scn, rp + 1, pa1);
-              }
-            }
-            f.steady_step(zq[cur], ybq[cur]);
-            // pin the step's results here: without a use the compiler sinks the whole mean-update chain
-            // past the block's end (it is only read by later blocks), away from the MFMAs it should hide
-#pragma unroll
-            for (int i = 0; i < M; ++i) asm volatile("" ::"v"(f.beta[i]));
-            asm volatile("" ::"v"(f.sumq), "v"(f.ld.mant));
-            // one scheduling region per step, the step's MFMAs spread through its mean update (the
-            // in-order wave would otherwise stall on the busy matrix pipe issuing them back to back)
-            const int MF = 2 * (((tt + 1) * U) / TB - (tt * U) / TB);
-#pragma unroll
-            for (int g = 0; g < MF; ++g) {
-              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);          // 1 MFMA
-              __builtin_amdgcn_sched_group_barrier(0x002, kPipeValu, 0);  // then VALU
-            }
-            __builtin_amdgcn_sched_barrier(0);
-          }
-          // the chunk rotation of the block's last step (t0 is a multiple of TB, so only t0 + TB − 1 can
-          // end a chunk; nothing in the block reads LDS past it): outside the unrolled steps, which stay one
-          // basic block — a branch inside would let the compiler sink the arithmetic below the MFMAs
-          rotate(t0 + TB - 1);
-          steady_steps += TB;
-          f.count_steady(TB);
-          have_next = true;
-        }
-      }
       if constexpr (STEADY) {
-        if (blk_steady && !have_next) {
+        if (blk_steady) {
           if (tend == TB) {
             // a whole block: the 16 steps unrolled into one basic block (no loop control or operand copies;
             // the chunk rotation, which only the block's last step can trigger, after it): 0.2114 → 0.2042 ms
@@ -951,20 +720,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
               ybq[nx] = *reinterpret_cast<const double2*>(cb + tn * LDP + NP);
               f.steady_step(zq[cur], ybq[cur]);
             }
-            if constexpr (LA) {
-              if (la_next) {  // the next block's z̃ (the D layout of the block form above), other buffer
-                double* scn = scratch[wave][buf ^ 1];
-#pragma unroll
-                for (int r = NRT / 2; r < NRT; ++r) store_tile(scn, r, la_acc[r]);
-              }
-            }
-            // RL: the rotation at the next block's start instead — with its barrier after the steps the compiler
-            // sinks the steps' arithmetic below it and issues all 32 operand reads up front (128 registers)
-            if constexpr (RL) {
-              rot_t = ((t0 + TB) % TC == 0) ? t0 + TB - 1 : -1;
-            } else {
-              rotate(t0 + TB - 1);
-            }
+            rot_t = ((t0 + TB) % TC == 0) ? t0 + TB - 1 : -1;  // at the next block's start
           } else {
             int tt = 0;
             for (; tt + 1 < tend; tt += 2) {
@@ -979,7 +735,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
       }
       if (!blk_steady) {
         int tt = 0;
-        bool rest_steady = false;  // MID: the rest of this block runs in the steady loop
+        bool rest_steady = false;  // the rest of this block runs in the steady loop
         for (; tt + 1 < tend; tt += 2) {
           half(tt, zc, yb, meta, zn, ybn, metan);
           half(tt + 1, zn, ybn, metan, zc, yb, meta);
@@ -987,7 +743,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
             // mid-block as well: lanes may freeze within this block (without it the config-2 steady share
             // drops 0.973 → 0.947, 0.226 → 0.234 ms; profiles/r4/exp1/)
             if (tt == TB / 2 - 2) f.prepare_bound();
-            if constexpr (MID) {
+            {
               // from the block's second half on, at every step pair: once every lane is frozen (the wave
               // vote of the block's end, taken early) and the rest of the block is data steps of every lane
               // with no NaN column, the remaining steps run as steady steps — the first block's waves freeze
@@ -1009,7 +765,7 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
             }
           }
         }
-        if constexpr (STEADY && MID) {
+        if constexpr (STEADY) {
           if (rest_steady) {  // step tt's operands are in (zc, yb): read ahead by the last `half`
             const int n = tend - tt;
             for (; tt + 1 < tend; tt += 2) {
@@ -1028,32 +784,8 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
       }
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();  // scratch reads done before the next block's writes
-#ifdef YFM_PHASE_PROBE
-      const long long ph_d = __builtin_readcyclecounter();
-      ph_bound += ph_a2 - ph_a;
-      ph_bload += ph_a3 - ph_a2;
-      ph_mfma += ph_b - ph_a3;
-      ph_dec += ph_c - ph_b;
-      if (blk_steady) {
-        ph_st += ph_d - ph_c;
-        ++ph_nst;
-      } else {
-        ph_full += ph_d - ph_c;
-        ++ph_nfull;
-      }
-#endif
-      if constexpr (PIPE) {
-        buf ^= 1;
-        have_z = have_next;
-      }
-      if constexpr (LA) {
-        have_z = la_next;
-        if (la_next) buf ^= 1;
-      }
     }
-    if constexpr (RL) {
-      if (rot_t >= 0) rotate(rot_t);  // every wave passes the same barriers
-    }
+    if (rot_t >= 0) rotate(rot_t);  // every wave passes the same barriers
     if constexpr (STEADY) {
       if (lane == 0 && steady_steps) atomicAdd(&flags[4], steady_steps);  // yfm_last_batch_steady
     }
@@ -1087,15 +819,6 @@ __global__ __launch_bounds__(kBlock, 1) void fixedz_loglik_kernel(
     if (t < nsteps) half(t, zc, yb_c, meta_c, zn, yb_n, meta_n);
   }
 
-#ifdef YFM_PHASE_PROBE
-  if (lane == 0 && (blockIdx.x % 64) == 0)
-    printf("setup blk %d wave %d decode %lld loadings+G %lld frag %lld filter-setup %lld rest %lld\n", (int)blockIdx.x,
-           wave, ph_s1 - ph_entry, ph_s2 - ph_s1, ph_s3 - ph_s2, ph_s4 - ph_s3, ph_t0 - ph_s4);
-  if (lane == 0 && (blockIdx.x % 64) == 0)
-    printf("phase blk %d wave %d loop %lld setup %lld bound %lld bload %lld mfma+st %lld dec %lld steady %lld (%d) full %lld (%d)\n",
-           (int)blockIdx.x, wave, (long long)__builtin_readcyclecounter() - ph_t0, ph_t0 - ph_entry, ph_bound, ph_bload,
-           ph_mfma, ph_dec, ph_st, ph_nst, ph_full, ph_nfull);
-#endif
   if (!live || defer) return;
   const double ll = f.loglik(nobs, flags);
   out[b] = ll;
@@ -1121,15 +844,6 @@ static int steady_enabled() {
 // the GNS5 steady state: off unless YFM_GNS5_STEADY=1
 static int gns5_steady_enabled() {
   const char* e = std::getenv("YFM_GNS5_STEADY");
-  return (e && e[0] == '1') ? 1 : 0;
-}
-
-// the pipelined steady blocks of the DNS kernel (PIPE): off unless YFM_DNS_PIPE=1.  FP64 MFMA and FP64
-// VALU share one pipe on gfx950 (tools/mfma_valu_overlap.hip: one MFMA wave + one VALU wave per SIMD take
-// the sum of their times), so the overlap can only fill latency bubbles: measured 0.2230 vs 0.2196 ms
-// without it on the final build (profiles/r4/exp2/)
-static int pipe_enabled() {
-  const char* e = std::getenv("YFM_DNS_PIPE");
   return (e && e[0] == '1') ? 1 : 0;
 }
 
@@ -1162,11 +876,6 @@ static hipError_t launch_fixedz_np(const LaunchArgs& a) {
     const bool on = steady_enabled() && a.T >= kSteadyMinT && (M != 5 || gns5_steady_enabled());
     auto* k = (kSteady && on) ? &fixedz_loglik_kernel<NP, M, LEAD, false, kSteady>
                               : &fixedz_loglik_kernel<NP, M, LEAD, false, false>;
-    // DNS: the steady blocks overlap the next block's Z'ỹ MFMAs with their mean updates (YFM_DNS_PIPE=1: on)
-    if constexpr (kSteady && M == 3) {
-      if (k == &fixedz_loglik_kernel<NP, M, LEAD, false, kSteady> && pipe_enabled())
-        k = &fixedz_loglik_kernel<NP, M, LEAD, false, kSteady, false, true>;
-    }
     // diagnostic: the two-function form of the update (commit 7a42719's regression test), GNS5 full recursion
     constexpr bool kSplitForm = (M == 5) && (NP == 30 || NP == 48);
     if constexpr (kSplitForm) {

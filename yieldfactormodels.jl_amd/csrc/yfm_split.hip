@@ -391,8 +391,7 @@ namespace {
 
 template <int NP>
 hipError_t launch_split_np(const LaunchArgs& a) {
-  const char* e = std::getenv("YFM_SPLIT_INTERLEAVE");  // wave-to-role layout (experiments)
-  const int interleave = (e && e[0] == '1') ? 1 : 0;
+  const int interleave = 0;  // wave-to-role layout: covariance waves 0-3, mean waves 4-7 (1: alternating)
   const int grid = (a.B + kSplitPairs * 64 - 1) / (kSplitPairs * 64);
   if (a.rec_beta) {
     hipLaunchKernelGGL((dns_split_kernel<NP, true>), dim3(grid), dim3(kSplitBlock), 0, a.stream, a.theta, a.P, a.B,

@@ -225,9 +225,6 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
   double sumq = 0.0;
   bool neg = false;
   double last_det = 0.0, last_q = 0.0;  // fresh model: F = 0, F⁻¹ = 0, v = 0 (kalmanbasemodel.jl:65-67)
-#if defined(YFM_TVL_PROBE) && YFM_TVL_PROBE == 2
-  bool probe_swapped = false;  // statistics probe: did partial pivoting ever exchange rows?
-#endif
 
   __syncthreads();
   const int nsteps = max(s_nobs_max, 0);
@@ -373,14 +370,6 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
       const double u[M] = {s[U1], s[U2], s[U3], s[U4]};
       const double vv = s[VV];
 
-#if defined(YFM_TVL_PROBE) && YFM_TVL_PROBE == 1
-      // timing probe only (tools/build_probe.sh): the 4×4 update replaced by a data-dependent no-op
-      double det = 1.0 + 1e-300 * (vv + G[3][3]);
-#pragma unroll
-      for (int i = 0; i < M; ++i) beta[i] = fma(1e-300, u[i], beta[i]);
-      const bool upd = true;
-      const double q = vv * rsig2;
-#else
       double det, q;
       bool upd;
       if constexpr (DIST) {
@@ -466,11 +455,7 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
         }
       } else {
       double W[M][M];
-#if defined(YFM_TVL_PROBE) && YFM_TVL_PROBE == 2
-      Capacitance<M>::solve(Pm, G, sigma2, W, det, &probe_swapped);  // statistics probe
-#else
       Capacitance<M>::solve(Pm, G, sigma2, W, det);
-#endif
 #pragma unroll
       for (int i = 0; i < M; ++i)
 #pragma unroll
@@ -492,7 +477,6 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
       upd = det != 0.0;  // inv(F) threw: return without updating (filter.jl:51-56)
       if (upd) propagate_state<M, 0>(p, bf, Pf, beta, Pm);
       }
-#endif
       last_det = det;
       last_q = upd ? q : __builtin_nan("");
       if (acc) {
@@ -526,9 +510,6 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
   }
 
   if (!live || j != 0) return;
-#if defined(YFM_TVL_PROBE) && YFM_TVL_PROBE == 2
-  if (probe_swapped) atomicAdd(&flags[0], 1u);  // statistics probe: filters that ever pivoted
-#endif
   double ll;
   if (!init_ok) {
     ll = __builtin_nan("");  // the reference throws from initialize_filter

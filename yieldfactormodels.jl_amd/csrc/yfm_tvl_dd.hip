@@ -27,21 +27,9 @@
 #include "yfm_device.hpp"
 #include "yfm_internal.hpp"
 
-#ifndef YFM_DD_SPLIT_Z4
-#define YFM_DD_SPLIT_Z4 1  // 0: TwoSum accumulation for the Jacobian-column sums (A/B builds)
-#endif
-// Per-maturity statistics in the moment basis (round 5): the lane accumulates
-// Σ z^a·c_i (a = 1, 2; c ∈ {1, 1/m, 1/m², m, m², y, y/m, y·m}) and the loading-basis sums (z2 = (1 − z)/(λm),
-// z4 = z·t) are formed per step from them — no per-maturity z2, 1/τ or Jacobian term.  0: the round-4 basis.
-#ifndef YFM_TVL_MOMENTS
-#define YFM_TVL_MOMENTS 0
-#endif
-
-// waves per SIMD the loglik kernel is compiled for (A/B builds: 2 caps it at 256 registers per lane, so that
-// L = 8 at config 3 runs two waves per SIMD)
-#ifndef YFM_TVL_DD_WAVES
-#define YFM_TVL_DD_WAVES 1
-#endif
+// Variants measured and not kept (in git history): the statistics in a moment basis Σ z^a·c_i
+// (−7% time, but the Jacobian-column sums cancel: 1.1e-8 from the binary128 truth), two waves per SIMD at L = 8
+// under a 256-register cap (24.8 vs 21.8 ms), TwoSum instead of σ-split accumulation of the Jacobian-column sums.
 
 namespace yfm {
 
@@ -280,34 +268,30 @@ __global__ __launch_bounds__(64) void tvl_dd_init_kernel(const double* __restric
 
 // Σ_i y_it and Σ_i y_it² per panel column in dd (summed in maturity order; NaN columns give
 // NaN and are never read): colsum[4t .. 4t+3] = (Σy.hi, Σy.lo, Σy².hi, Σy².lo); colsum[4T + t] =
-// max_i |y_it| (the bound of the σ-split statistics' y terms); colsum[5T + 2t .. +1] = Σ_i y_it/m_i (dd,
-// the moment basis's Σ y z2 = (Σ y/m − Σ y z/m)/λ)
+// max_i |y_it| (the bound of the σ-split statistics' y terms)
 __global__ __launch_bounds__(64) void tvl_dd_colsum_kernel(const double* __restrict__ Y, int N, int T,
-                                                           const double* __restrict__ mats, double* __restrict__ colsum) {
+                                                           double* __restrict__ colsum) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= T) return;
   const double* y = Y + (size_t)t * N;
-  dd_acc s1, s2, s3;
+  dd_acc s1, s2;
   double ym = 0.0;
   for (int i = 0; i < N; ++i) {
     const double v = y[i];
     s1.add(dd_make(v));
     s2.add(two_prod(v, v));
-    s3.add(dd_mul(dd_make(v), dd_rcp(dd_make(mats[i]))));
     ym = fmax(ym, fabs(v));
   }
   colsum[4 * (size_t)T + t] = ym;
-  const dd a = s1.value(), b = s2.value(), c = s3.value();
+  const dd a = s1.value(), b = s2.value();
   colsum[4 * (size_t)t] = a.hi;
   colsum[4 * (size_t)t + 1] = a.lo;
   colsum[4 * (size_t)t + 2] = b.hi;
   colsum[4 * (size_t)t + 3] = b.lo;
-  colsum[5 * (size_t)T + 2 * (size_t)t] = c.hi;
-  colsum[5 * (size_t)T + 2 * (size_t)t + 1] = c.lo;
 }
 
 template <int L, bool RECORD>
-__global__ __launch_bounds__(kDdBlock, YFM_TVL_DD_WAVES) void tvl_dd_loglik_kernel(
+__global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
     const double* __restrict__ rec, int B, const double* __restrict__ Y, const double* __restrict__ colsum,
     const double* __restrict__ prep, int ldp,
     int np, int T, int N, int TC, const double* __restrict__ mats, int K, const double* __restrict__ gap_d,
@@ -315,20 +299,17 @@ __global__ __launch_bounds__(kDdBlock, YFM_TVL_DD_WAVES) void tvl_dd_loglik_kern
     double* __restrict__ rec_P, int horizon, int rec_len) {
   constexpr int GPB = kDdBlock / L;
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  constexpr int kMom = YFM_TVL_MOMENTS ? 1 : 0;
-  constexpr int kSumDd = 2 + kMom;                     // dd column sums per staged column
+  constexpr int kSumDd = 2;                            // dd column sums per staged column
   double* s_m = smem;                                  // m_i
   dd* s_rm = reinterpret_cast<dd*>(smem + N);          // 1/m_i (dd)
-  dd* s_mc = reinterpret_cast<dd*>(smem + 3 * N);      // (moments) per maturity: 1/m², m² (dd)
-  double* s_nan = smem + (3 + 4 * kMom) * N;           // TC NaN flags of the staged chunk
-  dd* s_sum = reinterpret_cast<dd*>(s_nan + TC);       // per staged column: Σy, Σy² (, Σy/m) (dd)
+  double* s_nan = smem + 3 * N;                        // TC NaN flags of the staged chunk
+  dd* s_sum = reinterpret_cast<dd*>(s_nan + TC);       // per staged column: Σy, Σy² (dd)
   double* s_ymax = s_nan + (1 + 2 * kSumDd) * TC;      // per staged column: max_i |y_i|
   double* s_y = s_ymax + TC;                           // TC columns of N yields
   double* s_par = s_y + TC * N;                        // per group: σ², δ, Φ, Q (kDPar doubles)
   dd* s_w = reinterpret_cast<dd*>(s_par + GPB * kDPar);  // per group: e^{-λ d_k}, k < K
   dd* s_xch = s_w + GPB * kDdWStride;                  // per group: 4×4 dd exchange block
-  dd* s_cst = s_xch + GPB * M4 * M4;                   // (moments) per group: Σ1/m, Σ1/m² over all maturities
-  int* s_gi = reinterpret_cast<int*>(s_cst + 2 * kMom * GPB);
+  int* s_gi = reinterpret_cast<int*>(s_xch + GPB * M4 * M4);
   __shared__ double s_gd[kTvlGaps];
   __shared__ int s_gsrc[kTvlGaps];  // a lane whose first maturity equals jump k exactly, or −1
   __shared__ int s_nobs_max;
@@ -345,12 +326,7 @@ __global__ __launch_bounds__(kDdBlock, YFM_TVL_DD_WAVES) void tvl_dd_loglik_kern
   for (int i = tid; i < N; i += kDdBlock) {
     const double m = mats[i];
     s_m[i] = m;
-    const dd rm = dd_rcp(dd_make(m));
-    s_rm[i] = rm;
-    if constexpr (kMom) {
-      s_mc[2 * i] = dd_mul(rm, rm);     // 1/m²
-      s_mc[2 * i + 1] = two_prod(m, m);  // m² (exact)
-    }
+    s_rm[i] = dd_rcp(dd_make(m));
     if (K > 0) s_gi[i] = gap_idx[i];
   }
   if (tid < K) {
@@ -372,19 +348,6 @@ __global__ __launch_bounds__(kDdBlock, YFM_TVL_DD_WAVES) void tvl_dd_loglik_kern
     l_maxm = fmax(l_maxm, s_m[i]);
   }
   const double l_rminm = 1.0 / l_minm;
-  if constexpr (kMom) {
-    // this filter's Σ_i 1/m_i and Σ_i 1/m_i² (the constant parts of Σ z2 and Σ z2²), once
-    dd_acc a1, a2;
-    for (int i = j; i < N; i += L) {
-      a1.add(s_rm[i]);
-      a2.add(s_mc[2 * i]);
-    }
-    const dd c1 = group_sum_acc<L>(a1), c2 = group_sum_acc<L>(a2);
-    if (j == 0) {
-      s_cst[2 * grp] = c1;
-      s_cst[2 * grp + 1] = c2;
-    }
-  }
   const int my_steps = horizon > 0 ? nobs + horizon : nobs - 1;
   const int my_data = horizon > 0 ? nobs : nobs - 1;
   atomicMax(&s_nobs_max, live ? my_steps : 0);
@@ -429,10 +392,6 @@ __global__ __launch_bounds__(kDdBlock, YFM_TVL_DD_WAVES) void tvl_dd_loglik_kern
 #pragma unroll
     for (int q = 0; q < 4; ++q) pre_sum[q] = own ? colsum[(size_t)tc * 4 + q] : 0.0;
     pre_ymax = own ? colsum[(size_t)T * 4 + tc] : 0.0;
-    if constexpr (kMom) {
-      pre_sum[4] = own ? colsum[(size_t)T * 5 + 2 * (size_t)tc] : 0.0;
-      pre_sum[5] = own ? colsum[(size_t)T * 5 + 2 * (size_t)tc + 1] : 0.0;
-    }
   };
   auto store_chunk = [&]() {
 #pragma unroll
@@ -444,7 +403,6 @@ __global__ __launch_bounds__(kDdBlock, YFM_TVL_DD_WAVES) void tvl_dd_loglik_kern
       s_nan[tid] = pre_nan;
       s_sum[kSumDd * tid] = {pre_sum[0], pre_sum[1]};
       s_sum[kSumDd * tid + 1] = {pre_sum[2], pre_sum[3]};
-      if constexpr (kMom) s_sum[kSumDd * tid + 2] = {pre_sum[4], pre_sum[5]};
       s_ymax[tid] = pre_ymax;
     }
   };
@@ -495,57 +453,6 @@ __global__ __launch_bounds__(kDdBlock, YFM_TVL_DD_WAVES) void tvl_dd_loglik_kern
       // (yfm_dd.hpp: dd_acc::add_sx): per step and lane, a tight bound on the terms over this lane's
       // maturities (z = e^{−λm} ≤ e^{−λ m_min}, z2 = (1 − z)/(λm) ≤ min(1, 1/(λ m_min)), |y| ≤ the
       // column's max) fixes the split constant.
-#if YFM_TVL_MOMENTS
-      // Per maturity only z = e^{−λm} (the recurrence below) and z² enter, against constants of the maturity
-      // (1, 1/m, 1/m², m, m²) and of the panel (y, y/m, y·m): twelve moments M = Σ_i z_i^a c_i.  The
-      // loading-basis sums follow per step (z2 = (1 − z)/(λm), z4 = z·t, t = k1 − kr/m + c2·m):
-      //   Σz2 = (Σ1/m − Σz/m)/λ          Σz2² = (Σ1/m² − 2Σz/m² + Σz²/m²)/λ²     Σz2·z = (Σz/m − Σz²/m)/λ
-      //   Σz4 = k1Σz − krΣz/m + c2Σzm     Σz·z4 = k1Σz² − krΣz²/m + c2Σz²m
-      //   Σz2·z4 = (k1(Σz/m − Σz²/m) − kr(Σz/m² − Σz²/m²) + c2(Σz − Σz²))/λ
-      //   Σz4² = k1²Σz² + kr²Σz²/m² + c2²Σz²m² − 2k1krΣz²/m + 2k1c2Σz²m − 2krc2Σz²
-      //   Σy·z2 = (Σy/m − Σyz/m)/λ        Σy·z4 = k1Σyz − krΣyz/m + c2Σyzm
-      // The combinations cancel (at most ~10 bits on G22 and G44 for the grids and λ here): harmless in dd,
-      // which is why the FP64 kernel keeps the loading basis.  Every moment is a σ-split accumulation whose
-      // split constant comes from a tight per-lane, per-step bound of its terms (as the loading basis's).
-      const double lamh = lam.hi, rlh = rl.hi;
-      constexpr double kSlack = 1.0 + 0x1p-30;
-      const double Be = exp(-(lamh * l_minm)) * kSlack;  // z ≤ e^{−λ m_min}
-      const double Be2 = Be * Be * kSlack;
-      const double r1 = l_rminm * kSlack, r2 = l_rminm * l_rminm * kSlack;
-      // max over m ≥ m_min of m·e^{−λm} (peak at 1/λ), m·e^{−2λm} (1/(2λ)), m²·e^{−2λm} (1/λ)
-      const double Bem = (lamh * l_minm >= 1.0 ? Be * l_minm : 0.36787944117144233 * rlh) * kSlack;
-      const double Bqm = (2.0 * lamh * l_minm >= 1.0 ? Be2 * l_minm : 0.18393972058572117 * rlh) * kSlack;
-      const double Bqq = (lamh * l_minm >= 1.0 ? Be2 * l_minm * l_minm : 0.1353352832366127 * rlh * rlh) * kSlack;
-      const double By = s_ymax[tt] * l_n;
-      const double sz0 = split_const(l_n * Be), sz1 = split_const(l_n * Be * r1), sz2 = split_const(l_n * Be * r2);
-      const double szm = split_const(l_n * Bem);
-      const double sq0 = split_const(l_n * Be2), sq1 = split_const(l_n * Be2 * r1), sq2 = split_const(l_n * Be2 * r2);
-      const double sqm = split_const(l_n * Bqm), sqq = split_const(l_n * Bqq);
-      const double sy0 = split_const(By * Be), sy1 = split_const(By * Be * r1), sym = split_const(By * Bem);
-      dd_acc Mz0, Mz1, Mz2, Mzm, Mq0, Mq1, Mq2, Mqm, Mqq, My0, My1, Mym;
-      auto accum = [&](int i, dd z) {
-        const double m = s_m[i];
-        const double y = col[i];
-        const dd rm = s_rm[i], rm2 = s_mc[2 * i], m2 = s_mc[2 * i + 1];
-        const dd zz = dd_mul_nn(z, z);
-        // y/m and y·m (y a double): left unnormalised, they only feed the σ-split products
-        dd yrm = two_prod(y, rm.hi);
-        yrm.lo = __builtin_fma(y, rm.lo, yrm.lo);
-        const dd ym = two_prod(y, m);
-        Mz0.add_sx(z, sz0);
-        Mz1.add_prod_sx(z, rm, sz1);
-        Mz2.add_prod_sx(z, rm2, sz2);
-        Mzm.add_prod_d_sx(z, m, szm);
-        Mq0.add_sx(zz, sq0);
-        Mq1.add_prod_sx(zz, rm, sq1);
-        Mq2.add_prod_sx(zz, rm2, sq2);
-        Mqm.add_prod_d_sx(zz, m, sqm);
-        Mqq.add_prod_sx(zz, m2, sqq);
-        My0.add_prod_d_sx(z, y, sy0);
-        My1.add_prod_sx(z, yrm, sy1);
-        Mym.add_prod_sx(z, ym, sym);
-      };
-#else
       const double lamh = lam.hi, rlh = rl.hi;
       constexpr double kSlack = 1.0 + 0x1p-30;
       const double Be = exp(-(lamh * l_minm)) * kSlack;
@@ -555,13 +462,11 @@ __global__ __launch_bounds__(kDdBlock, YFM_TVL_DD_WAVES) void tvl_dd_loglik_kern
       const double sgt = split_const((fabs(k1.hi) + fabs(kr.hi) * l_rminm + fabs(c2.hi) * l_maxm) * kSlack);
       const double qk1 = (sgt + k1.hi) - sgt;
       const double rk1 = (k1.hi - qk1) + k1.lo;
-#if YFM_DD_SPLIT_Z4
       const double Bem = (lamh * l_minm >= 1.0 ? Be * l_minm : 0.36787944117144233 * rlh) * kSlack;
       const double B4 = (Be * (fabs(k1.hi) + fabs(kr.hi) * l_rminm) + fabs(c2.hi) * Bem) * kSlack;
       const double sg4 = split_const(l_n * B4), sg24 = split_const(l_n * Bz2 * B4);
       const double sgz4 = split_const(l_n * Be * B4), sg44 = split_const(l_n * B4 * B4);
       const double sy4 = split_const(By * B4);
-#endif
       const double sg2 = split_const(l_n * Bz2), sgz = split_const(l_n * Be);
       const double sg22 = split_const(l_n * Bz2 * Bz2), sg2z = split_const(l_n * Bz2 * Be);
       const double sgzz = split_const(l_n * Be * Be);
@@ -595,23 +500,12 @@ __global__ __launch_bounds__(kDdBlock, YFM_TVL_DD_WAVES) void tvl_dd_loglik_kern
         Gzz.add_prod_sx(z, z, sgzz);
         Y2.add_prod_d_sx(z2, y, sy2);
         Yz.add_prod_d_sx(z, y, syz);
-#if YFM_DD_SPLIT_Z4
         S4.add_sx(z4, sg4);
         G24.add_prod_sx(z2, z4, sg24);
         Gz4.add_prod_sx(z, z4, sgz4);
         G44.add_prod_sx(z4, z4, sg44);
         Y4.add_prod_d_sx(z4, y, sy4);
-#else
-        // the Jacobian-column sums keep TwoSum accumulation (|z4| has no tight per-lane bound:
-        // t = k1(1 − 1/τ) + c2·m cancels near λm = 1)
-        S4.add(z4);
-        G24.add_prod(z2, z4);
-        Gz4.add_prod(z, z4);
-        G44.add_prod(z4, z4);
-        Y4.add_prod_d(z4, y);
-#endif
       };
-#endif
       if (K > 0) {
         dd* w = s_w + grp * kDdWStride;
         dd z = (j < N) ? dd_exp(neg_rate(lam, s_m[j])) : dd_make(0.0);
@@ -632,59 +526,10 @@ __global__ __launch_bounds__(kDdBlock, YFM_TVL_DD_WAVES) void tvl_dd_loglik_kern
       } else {
         for (int i = j; i < N; i += L) accum(i, dd_exp(neg_rate(lam, s_m[i])));
       }
-#if YFM_TVL_MOMENTS
-      const dd mz0 = group_sum_acc<L>(Mz0), mz1 = group_sum_acc<L>(Mz1), mz2 = group_sum_acc<L>(Mz2);
-      const dd mzm = group_sum_acc<L>(Mzm), mq0 = group_sum_acc<L>(Mq0), mq1 = group_sum_acc<L>(Mq1);
-      const dd mq2 = group_sum_acc<L>(Mq2), mqm = group_sum_acc<L>(Mqm), mqq = group_sum_acc<L>(Mqq);
-      const dd my0 = group_sum_acc<L>(My0), my1 = group_sum_acc<L>(My1), mym = group_sum_acc<L>(Mym);
-      const dd cs1 = s_cst[2 * grp], cs2 = s_cst[2 * grp + 1];
-      const dd nkr = dd_neg(kr);
-      auto lin3 = [&](dd a, dd x, dd b, dd y_, dd c, dd w) {  // a·x + b·y + c·w
-        dd_acc acc_;
-        acc_.add_prod(a, x);
-        acc_.add_prod(b, y_);
-        acc_.add_prod(c, w);
-        return acc_.value();
-      };
-      // every z underflowed (λ near the FP64 range): the Jacobian-column sums are Σ 0·t = 0 as in the loading
-      // basis, where the coefficient products (c2², k1·c2, …) could overflow and give Inf·0 = NaN
-      const bool znone = mz0.hi == 0.0;
-      const dd zero = dd_make(0.0);
-      const dd d1 = dd_sub(mz1, mq1), d2 = dd_sub(mz2, mq2), d0 = dd_sub(mz0, mq0);
-      const dd s2 = dd_mul(rl, dd_sub(cs1, mz1));
-      const dd sz = mz0;
-      const dd s4 = znone ? zero : lin3(k1, mz0, nkr, mz1, c2, mzm);
-      const dd g22 = dd_mul(dd_mul(rl, rl), dd_add(dd_sub(cs2, dd_ldexp(mz2, 1)), mq2));
-      const dd g2z = dd_mul(rl, d1);
-      const dd g24 = znone ? zero : dd_mul(rl, lin3(k1, d1, nkr, d2, c2, d0));
-      const dd gzz = mq0;
-      const dd gz4 = znone ? zero : lin3(k1, mq0, nkr, mq1, c2, mqm);
-      dd g44;
-      {
-        dd_acc a;
-        a.add_prod(dd_mul(k1, k1), mq0);
-        a.add_prod(dd_mul(kr, kr), mq2);
-        a.add_prod(dd_mul(c2, c2), mqq);
-        a.add_prod(dd_ldexp(dd_mul(k1, nkr), 1), mq1);
-        a.add_prod(dd_ldexp(dd_mul(k1, c2), 1), mqm);
-        a.add_prod(dd_ldexp(dd_mul(nkr, c2), 1), mq0);
-        g44 = znone ? zero : a.value();
-      }
-      const dd y2 = dd_mul(rl, dd_sub(s_sum[kSumDd * tt + 2], my1));
-      const dd yz = my0;
-      const dd y4 = znone ? zero : lin3(k1, my0, nkr, my1, c2, mym);
-#else
       const dd s2 = group_sum_acc<L>(S2), sz = group_sum_acc<L>(Sz), s4 = group_sum_acc<L>(S4);
       const dd g22 = group_sum_acc<L>(G22), g2z = group_sum_acc<L>(G2z), g24 = group_sum_acc<L>(G24);
       const dd gzz = group_sum_acc<L>(Gzz), gz4 = group_sum_acc<L>(Gz4), g44 = group_sum_acc<L>(G44);
       const dd y2 = group_sum_acc<L>(Y2), yz = group_sum_acc<L>(Yz), y4 = group_sum_acc<L>(Y4);
-#endif
-#ifdef YFM_TVL_DUMP  // diagnostic builds only: the per-step loading-basis sums of filter 0
-      if (blockIdx.x == 0 && tid == 0 && t < YFM_TVL_DUMP)
-        printf("dump t %d lam %.17g %.17g s2 %.17g %.17g sz %.17g %.17g s4 %.17g %.17g g22 %.17g %.17g g2z %.17g %.17g g24 %.17g %.17g gzz %.17g %.17g gz4 %.17g %.17g g44 %.17g %.17g y2 %.17g %.17g yz %.17g %.17g y4 %.17g %.17g\n",
-               t, lam.hi, lam.lo, s2.hi, s2.lo, sz.hi, sz.lo, s4.hi, s4.lo, g22.hi, g22.lo, g2z.hi, g2z.lo, g24.hi, g24.lo,
-               gzz.hi, gzz.lo, gz4.hi, gz4.lo, g44.hi, g44.lo, y2.hi, y2.lo, yz.hi, yz.lo, y4.hi, y4.lo);
-#endif
       // back to the loading basis (1, z2, z3 = z2 − z, z4)
       const dd g23 = dd_sub(g22, g2z);
       dd G[M4][M4];
@@ -723,14 +568,6 @@ __global__ __launch_bounds__(kDdBlock, YFM_TVL_DD_WAVES) void tvl_dd_loglik_kern
         vv = a.value();
       }
 
-#if defined(YFM_TVL_PROBE) && YFM_TVL_PROBE == 1
-      // timing probe only (tools/build_probe.sh): the 4×4 update replaced by a data-dependent no-op
-#pragma unroll
-      for (int i = 0; i < M4; ++i) beta[i] = dd_add(beta[i], dd_ldexp(u[i], -1000));
-      const double q = dd_to_double(dd_mul(vv, rsig2));
-      const double dh = 1.0 + 1e-300 * G[3][3].hi;
-      const bool upd = true;
-#else
       // ---- capacitance solve: B̃ = σ²I + P G, W = B̃⁻¹P, distributed over the quad:
       // role qr forms row qr of B̃ (P symmetric: its row qr is the column it holds), every lane
       // factorises the broadcast B̃ and solves for ONE right-hand side, column qr of P ----
@@ -788,7 +625,6 @@ __global__ __launch_bounds__(kDdBlock, YFM_TVL_DD_WAVES) void tvl_dd_loglik_kern
         gather_sym(ws, Wf);
         dd_propagate_q(par, qr, bf, Wf, true, xch, beta, Pc);
       }
-#endif
       last_ld = upd ? log(fabs(dh)) : -__builtin_inf();
       last_q = upd ? q : __builtin_nan("");
       last_neg = dh < 0.0;
@@ -852,13 +688,11 @@ template <int L>
 hipError_t launch_tvl_dd_l(const LaunchArgs& a, const double* rec_dd, const TvlGaps& g, int TC) {
   constexpr int GPB = kDdBlock / L;
   const int grid = (a.B + GPB - 1) / GPB;
-  constexpr int kMom = YFM_TVL_MOMENTS ? 1 : 0;
-  constexpr int kSumDd = 2 + kMom;
-  // the kernel's LDS layout: m, 1/m, (1/m², m²), per staged column NaN flag, dd sums, max|y| and N yields,
-  // per group the parameters, jump factors, exchange block (and Σ1/m, Σ1/m²), and the jump index per maturity
-  const size_t shmem = sizeof(double) * (size_t)((3 + 4 * kMom) * a.N + (2 + 2 * kSumDd) * TC + TC * a.N +
-                                                 GPB * kDPar + 2 * GPB * kDdWStride + 2 * GPB * M4 * M4 +
-                                                 4 * kMom * GPB) +
+  constexpr int kSumDd = 2;
+  // the kernel's LDS layout: m, 1/m, per staged column NaN flag, dd sums, max|y| and N yields, per group the
+  // parameters, jump factors and exchange block, and the jump index per maturity
+  const size_t shmem = sizeof(double) * (size_t)(3 * a.N + (2 + 2 * kSumDd) * TC + TC * a.N + GPB * kDPar +
+                                                 2 * GPB * kDdWStride + 2 * GPB * M4 * M4) +
                        sizeof(int) * a.N;
   if (shmem > 160 * 1024) return hipErrorInvalidValue;  // gfx950: 160 KiB of LDS per workgroup
   auto* k = a.rec_beta ? &tvl_dd_loglik_kernel<L, true> : &tvl_dd_loglik_kernel<L, false>;
@@ -877,9 +711,9 @@ hipError_t launch_tvl_dd_l(const LaunchArgs& a, const double* rec_dd, const TvlG
 
 }  // namespace
 
-// per-candidate records, then the panel's column statistics (7 doubles per column: tvl_dd_colsum_kernel)
+// per-candidate records, then the panel's column statistics (5 doubles per column: tvl_dd_colsum_kernel)
 size_t tvl_dd_scratch_bytes(int B, int T) {
-  return sizeof(double) * ((size_t)kDRecLen * (size_t)(B > 0 ? B : 1) + 7 * (size_t)(T > 0 ? T : 1));
+  return sizeof(double) * ((size_t)kDRecLen * (size_t)(B > 0 ? B : 1) + 5 * (size_t)(T > 0 ? T : 1));
 }
 
 int tvl_dd_lanes_for(int B, int N, int want) {
@@ -902,7 +736,7 @@ int tvl_dd_lanes_for(int B, int N, int want) {
 hipError_t launch_tvl_dd_init(const LaunchArgs& a, double* rec_dd) {
   hipLaunchKernelGGL(tvl_dd_init_kernel, dim3((a.B + 63) / 64), dim3(64), 0, a.stream, a.theta, a.P, a.B, a.space,
                      rec_dd, a.flags_next);
-  hipLaunchKernelGGL(tvl_dd_colsum_kernel, dim3((a.T + 63) / 64), dim3(64), 0, a.stream, a.raw, a.N, a.T, a.mats,
+  hipLaunchKernelGGL(tvl_dd_colsum_kernel, dim3((a.T + 63) / 64), dim3(64), 0, a.stream, a.raw, a.N, a.T,
                      rec_dd + (size_t)kDRecLen * (size_t)(a.B > 0 ? a.B : 1));
   return hipGetLastError();
 }

@@ -139,12 +139,17 @@ def _rank(group) -> int:
     return dist.get_rank(group)
 
 
-def _broadcast_from_lead(arr, group) -> np.ndarray:
-    """Rank 0's array on every rank of `group` (a pickled object broadcast; a few hundred bytes)."""
+def _broadcast_obj(obj, group):
+    """Rank 0's object on every rank of `group` (a pickled object broadcast; a few hundred bytes)."""
     import torch.distributed as dist
-    box = [arr]
+    box = [obj]
     dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
-    return np.array(box[0], dtype=np.float64)
+    return box[0]
+
+
+def _broadcast_from_lead(arr, group) -> np.ndarray:
+    """Rank 0's array on every rank of `group`."""
+    return np.array(_broadcast_obj(arr, group), dtype=np.float64)
 
 
 def run(thread_id: str = "1", in_sample_end: int = 100, forecast_horizon: int = 12, run_rolling: bool = True,
@@ -172,8 +177,8 @@ def run(thread_id: str = "1", in_sample_end: int = 100, forecast_horizon: int = 
                                      results_location=f"{results_location}{model_type}/")
     param_groups = get_param_groups(model, param_groups)
     # With a group, rank 0 alone reads (or writes) the init file and every file below; the start is then
-    # broadcast, so no rank reads a file another one is still writing (the estimation before the rolling
-    # forecasts is deterministic: every rank computes the same parameters, only rank 0 saves them).
+    # broadcast, so no rank reads a file another one is still writing; the in-sample estimation runs on rank 0
+    # and its result is broadcast too.
     lead = group is None or _rank(group) == 0
     all_params = None
     if lead:
@@ -188,9 +193,19 @@ def run(thread_id: str = "1", in_sample_end: int = 100, forecast_horizon: int = 
     all_params[:, 0] = load_static_parameters_(model, model_type, results_location, thread_id, all_params[:, 0])
     info = {"files": []}
     if run_optimization:
-        print("The param groups are : ", param_groups)
-        init_params, loss, params, ir = run_estimation_(model, data, in_sample_end, all_params, param_groups,
-                                                        max_group_iters, group_tol, iterations=iterations)
+        # the in-sample estimation runs on the lead rank only; the other ranks take its result (every
+        # rank used to run the whole NelderMead and discard it, relying on bitwise-equal results across devices)
+        est = None
+        if lead:
+            print("The param groups are : ", param_groups)
+            est = run_estimation_(model, data, in_sample_end, all_params, param_groups, max_group_iters, group_tol,
+                                  iterations=iterations)
+            est = (np.asarray(est[0], dtype=np.float64), float(est[1]), np.asarray(est[2], dtype=np.float64),
+                   est[3])
+        if group is not None:
+            est = _broadcast_obj(est, group)
+        init_params, loss, params, ir = est
+        set_params_(model, params)  # as run_estimation_ leaves the lead's model
     else:
         init_params = params = all_params[:, 0].copy()
         loss, ir = 0.0, 0.0
