@@ -143,7 +143,9 @@ def make_workload(config: int, world: int, rank: int, T: int, batch: int | None)
                         S.simulate_panel(KIND_TVL, T, maturities=mats), Th, None, world * B, "weak", True)
     if config == 4:
         per = batch or 4096
-        wins = np.arange(361, 601) if T == 600 else np.arange(max(2, T - 239), T + 1)
+        # the windows longest first: waves run in rounds of one per SIMD, so the last, partial round holds the
+        # shortest windows (longest-processing-time-first; at 8 GPUs a rank's 1,920 waves take 1.875 rounds)
+        wins = np.arange(600, 360, -1) if T == 600 else np.arange(T, max(2, T - 239) - 1, -1)
         counts = [per] * len(wins)
         idx = D.window_shards(counts, world, rank)
         Th_all = S.theta_batch(KIND_DNS, per, seed=S.BATCH_SEED)  # the same 4,096 θ re-fit per window
@@ -152,7 +154,8 @@ def make_workload(config: int, world: int, rank: int, T: int, batch: int | None)
         mats = S.maturities_30()
         return Workload(4, KIND_DNS, f"config4: DNS rolling windows, {len(wins)} expanding windows × {per:,} θ "
                         f"= {len(wins) * per:,} evals split over {world} GPU(s)", mats, S.simulate_panel(KIND_DNS, T),
-                        Th, tu, len(wins) * per, "strong", True, {"windows": [int(wins[0]), int(wins[-1])]},
+                        Th, tu, len(wins) * per, "strong", True,
+                        {"windows": [int(wins.min()), int(wins.max())], "window_order": "longest first"},
                         [len(D.window_shards(counts, world, r)) for r in range(world)])
     if config == 5:
         total = batch or 1 << 20
@@ -406,6 +409,74 @@ def roofline(kind, prec, N, M, T, T_use, B, P, kernel_ms, steady_lane_steps=0):
                        else "")}
 
 
+def emulate_world(args) -> dict:
+    """Predict the N-GPU efficiency of a configuration from ONE GPU: build every rank's shard of world W exactly as
+    make_workload does for that rank and time it alone (HIP events around `steps` launches after `warmup`), then
+    the whole workload at world 1.  Strong scaling (configs 4, 5): predicted_efficiency = T₁ / (W · max_R T_R) —
+    the slowest rank's filter time sets the step; the collectives are not included (bench.py overlaps step k's
+    RCCL all-gather / argmax with step k+1's filter on separate streams).  Weak scaling (configs 2, 3): every rank
+    runs a full per-GPU batch, predicted_efficiency = T_rank0 / max_R T_R."""
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    eng = Engine(0)
+    eng.precision = {"certified": _lib.PREC_CERTIFIED, "fp64": _lib.PREC_FP64}[args.precision]
+    W = args.emulate_world
+    ranks = list(range(W)) if args.emulate_rank is None else [args.emulate_rank]
+    stream = torch.cuda.Stream(dev)
+
+    def time_shard(w: Workload) -> dict:
+        kind = w.kind
+        P, B = n_params(kind), w.Theta.shape[1]
+        eng.set_panel(w.Y, w.mats)
+        d_th = torch.from_numpy(np.ascontiguousarray(w.Theta.T)).to(dev)
+        d_tu = torch.from_numpy(w.T_use).to(dev) if w.T_use is not None else None
+        d_out = torch.empty(B, dtype=torch.float64, device=dev)
+
+        def launch():
+            eng.loglik_device(kind, d_th.data_ptr(), P, B, d_out.data_ptr(), space=0,
+                              d_T_use=d_tu.data_ptr() if d_tu is not None else None, stream=stream.cuda_stream)
+        t_end = time.perf_counter() + args.settle_seconds
+        while time.perf_counter() < t_end:  # the card's steady clock, as the timed region of main()
+            launch()
+            stream.synchronize()
+        for _ in range(args.warmup):
+            launch()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+        for a, b in ev:
+            a.record(stream)
+            launch()
+            b.record(stream)
+        stream.synchronize()
+        ms = [a.elapsed_time(b) for a, b in ev]
+        Tb = w.T_use if w.T_use is not None else np.full(B, w.Y.shape[1])
+        waves = -(-B // 64) if kind != KIND_TVL else None  # fixed loadings: one candidate per lane
+        return {"batch": int(B), "filter_steps": int(np.sum(np.asarray(Tb, dtype=np.int64) - 1)),
+                "kernel_ms_mean": float(np.mean(ms)), "kernel_ms_min": float(np.min(ms)),
+                "waves": waves, "waves_per_simd": waves / 1024.0 if waves else None,
+                "logliks_finite": int(torch.isfinite(d_out).sum().item())}
+
+    full = time_shard(make_workload(args.config, 1, 0, args.T, args.batch))
+    shards = {r: time_shard(make_workload(args.config, W, r, args.T, args.batch)) for r in ranks}
+    w0 = make_workload(args.config, W, 0, args.T, args.batch)
+    t_max = max(s["kernel_ms_mean"] for s in shards.values())
+    if w0.scaling == "strong":
+        pred = full["kernel_ms_mean"] / (W * t_max)
+        rule = "T_1 / (W · max_R T_R): the whole workload on one GPU against W× the slowest rank's shard"
+    else:
+        pred = shards[min(shards)]["kernel_ms_mean"] / t_max
+        rule = "weak scaling: every rank a full per-GPU batch; T_rank0 / max_R T_R"
+    return {"metric": f"predicted {W}-GPU scaling efficiency (config {args.config}, emulated on one GPU)",
+            "config": args.config, "workload": w0.label, "scaling": w0.scaling, "emulated_world": W,
+            "world1": full, "ranks": {str(r): s for r, s in shards.items()},
+            "max_rank_kernel_ms": t_max,
+            "rank_imbalance": t_max / min(s["kernel_ms_mean"] for s in shards.values()),
+            "predicted_efficiency": pred, "rule": rule, "steps": args.steps, "warmup": args.warmup,
+            "note": "kernel_ms = HIP events around each whole loglik call on its stream (init + filter + deferral "
+                    "kernels); collectives excluded (overlapped with the next step's filter in main()); the "
+                    "fixed-loading kernels run one wave per SIMD (1,024 per MI355X), so waves_per_simd above an "
+                    "integer leaves a partial last round of waves"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -426,8 +497,15 @@ def main():
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl = RCCL over xGMI (one GPU per rank); gloo = host collectives, ranks may share a GPU "
                          "(multi-rank rehearsal on a one-GPU box)")
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="predict the W-GPU efficiency on one GPU: time every rank's shard of world W alone "
+                         "(emulate_world); prints one JSON line and exits")
+    ap.add_argument("--emulate-rank", type=int, default=None, help="with --emulate-world: time this rank only")
     args = ap.parse_args()
 
+    if args.emulate_world > 1:
+        print(json.dumps(emulate_world(args)), flush=True)
+        return
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # no launcher: start the N ranks here (this parent never touches the GPU) and exit with their status
         sys.exit(D.spawn_local_ranks(str(Path(__file__).resolve()), sys.argv[1:], args.gpus,

@@ -236,6 +236,31 @@ def test_tvl_full_batch_properties(engine, config3):
     assert np.array_equal(np.isfinite(f), np.isfinite(a)) and np.array_equal(np.isnan(f), np.isnan(a))
 
 
+@pytest.mark.parametrize("L", [4, 8, 16, 32])
+def test_tvl_power_mode_wu30_t600(engine, L):
+    """The certified kernel's power mode (the N = 30 grid has 12–13 distinct jumps at L ≥ 4, more than the exact
+    jump table holds: e^{−λm} = (e^{−λΔ})^{m/Δ}, Δ = 3 months, one dd exp per step) against one dd exp per
+    maturity (YFM_TVL_EXP=1), at T = 600 on 64 candidates: both at factor 1 against the dense oracle and the
+    binary128 truth, and the power mode within 4× the per-maturity path's own distance from the truth (+1e-13)."""
+    mats = S.maturities_30()
+    Y = S.simulate_panel(KIND_TVL, 600, maturities=mats)
+    Th = S.theta_batch(KIND_TVL, 64, seed=47, bad_frac=0.0, scale=0.02)
+    engine.set_panel(Y, mats)
+    with env(YFM_TVL_LANES=L):
+        pw = engine.loglik(KIND_TVL, Th)
+        with env(YFM_TVL_EXP=1):
+            ex = engine.loglik(KIND_TVL, Th)
+    ref = loglik_oracle(KIND_TVL, Y, mats, Th)
+    truth = loglik_truth(KIND_TVL, Y, mats, Th)
+    for got in (pw, ex):
+        assert_parity(got, ref, truth)
+    e_pw, e_ex = rel(pw, truth), rel(ex, truth)
+    print(f"L {L}: power mode vs truth max {e_pw.max():.2e} (median {np.median(e_pw):.2e}); one exp per maturity "
+          f"{e_ex.max():.2e}; above 1e-13: {int((e_pw > EXACT).sum())} / {int((e_ex > EXACT).sum())}")
+    assert e_pw.max() <= 4.0 * e_ex.max() + EXACT
+    assert int((e_pw > EXACT).sum()) <= int((e_ex > EXACT).sum()) + 1
+
+
 @pytest.mark.parametrize("grid", ["wu30", "irregular"])
 def test_tvl_maturity_grids_and_exp_paths(engine, grid):
     """The exp recurrence over maturity jumps (≤ 8 distinct m_{i+L} − m_i) vs one exp per maturity

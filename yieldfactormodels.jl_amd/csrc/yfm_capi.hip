@@ -85,6 +85,7 @@ struct yfm::Workspace {
 struct yfm_ctx {
   int device = 0;
   int precision = YFM_PREC_CERTIFIED;  // TVλ arithmetic (yfm_set_precision)
+  int lane_share = 1;                  // concurrent launches in flight (yfm::set_lane_share)
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;  // θ uploads of pipelined host-pointer batches (created lazily)
   // panel
@@ -107,6 +108,9 @@ struct yfm_ctx {
   int gap_K[7] = {-1, -1, -1, -1, -1, -1, -1};
   bool gap_exact[7] = {};
   DevBuf gap_buf[7];
+  int pow_K[7] = {};       // power-mode tables (TvlGaps::Kp), built with the jump tables
+  double pow_step = 0.0;   // Δ (0: the maturities are not integer multiples of one step)
+  DevBuf pow_buf[7];
 };
 
 namespace {
@@ -178,6 +182,48 @@ int tvl_gaps(yfm_ctx* ctx, int L, yfm::TvlGaps& g) {
     }
     ctx->gap_K[l] = K;
     ctx->gap_exact[l] = exact;
+    // power mode: every maturity an integer multiple of Δ = gcd (exactly, as doubles: integer-valued and < 2^31)
+    ctx->pow_K[l] = 0;
+    long long gcd = 0;
+    bool integral = N > 0;
+    for (int i = 0; i < N && integral; ++i) {
+      const double m = ctx->mats_host[i];
+      integral = m > 0.0 && m < 2147483648.0 && m == std::floor(m);
+      long long a = integral ? (long long)m : 0, b = gcd;
+      while (b) {
+        const long long t = a % b;
+        a = b;
+        b = t;
+      }
+      gcd = a;
+    }
+    ctx->pow_step = integral ? (double)gcd : 0.0;
+    if (integral && N > L) {
+      std::vector<double> e;
+      std::vector<int> pidx(N, 0);
+      bool fits = true;
+      for (int i = 0; i + L < N && fits; ++i) {
+        const double q = (ctx->mats_host[i + L] - ctx->mats_host[i]) / (double)gcd;  // exact: integers < 2^31
+        int k = 0;
+        while (k < (int)e.size() && e[k] != q) ++k;
+        if (k == (int)e.size()) {
+          if ((int)e.size() == yfm::kTvlPowGaps || !(q >= 1.0 && q < 512.0)) fits = false;
+          else e.push_back(q);
+        }
+        pidx[i] = k;
+      }
+      if (fits) {
+        e.resize(yfm::kTvlPowGaps, 0.0);
+        YFM_HIP_CHECK(ctx->pow_buf[l].ensure(sizeof(double) * yfm::kTvlPowGaps + sizeof(int) * N));
+        char* base = static_cast<char*>(ctx->pow_buf[l].p);
+        YFM_HIP_CHECK(hipMemcpy(base, e.data(), sizeof(double) * yfm::kTvlPowGaps, hipMemcpyHostToDevice));
+        YFM_HIP_CHECK(hipMemcpy(base + sizeof(double) * yfm::kTvlPowGaps, pidx.data(), sizeof(int) * N,
+                                hipMemcpyHostToDevice));
+        int Kp = 0;
+        while (Kp < yfm::kTvlPowGaps && e[Kp] != 0.0) ++Kp;
+        ctx->pow_K[l] = Kp;
+      }
+    }
   }
   g.K = ctx->gap_K[l];
   g.exact = ctx->gap_exact[l];
@@ -186,8 +232,15 @@ int tvl_gaps(yfm_ctx* ctx, int L, yfm::TvlGaps& g) {
     g.d = reinterpret_cast<const double*>(base);
     g.idx = reinterpret_cast<const int*>(base + sizeof(double) * yfm::kTvlGaps);
   }
+  g.Kp = ctx->pow_K[l];
+  if (g.Kp > 0) {
+    char* base = static_cast<char*>(ctx->pow_buf[l].p);
+    g.step = ctx->pow_step;
+    g.e = reinterpret_cast<const double*>(base);
+    g.pidx = reinterpret_cast<const int*>(base + sizeof(double) * yfm::kTvlPowGaps);
+  }
   if (const char* ov = std::getenv("YFM_TVL_EXP")) {  // diagnostic: force one exp per maturity
-    if (std::atoi(ov) == 1) g.K = 0;
+    if (std::atoi(ov) == 1) g.K = g.Kp = 0;
   }
   return YFM_OK;
 }
@@ -289,14 +342,14 @@ int launch_impl(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P,
   a.stream = s;
   hipError_t e;
   if (kind == YFM_MODEL_TVL) {
-    int lanes = yfm::tvl_lanes_for(B, ctx->N);
+    int lanes = yfm::tvl_lanes_for(B, ctx->N, ctx->lane_share);
     if (const char* ov = std::getenv("YFM_TVL_LANES")) {  // tuning override: 1, 2, 4, …, 64
       const int l = std::atoi(ov);
       if (l >= 1 && l <= 64 && (l & (l - 1)) == 0) lanes = l;
     }
     yfm::TvlGaps g;
     if (ctx->precision == YFM_PREC_CERTIFIED) {
-      lanes = yfm::tvl_dd_lanes_for(B, ctx->N, std::getenv("YFM_TVL_LANES") ? lanes : 0);
+      lanes = yfm::tvl_dd_lanes_for(B, ctx->N, std::getenv("YFM_TVL_LANES") ? lanes : 0, ctx->lane_share);
       YFM_HIP_CHECK(w_scratch_dd.ensure(yfm::tvl_dd_scratch_bytes(B, a.T)));
       double* rdd = static_cast<double*>(w_scratch_dd.p);
       if (int r = tvl_gaps(ctx, lanes, g)) return r;
@@ -455,6 +508,7 @@ void yfm_destroy(yfm_ctx* ctx) {
     b->release();
   ctx->scratch_dd.release();
   for (DevBuf& b : ctx->gap_buf) b.release();
+  for (DevBuf& b : ctx->pow_buf) b.release();
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
   delete ctx;
@@ -786,6 +840,10 @@ int loglik_device_ws(yfm_ctx* ctx, Workspace* ws, int kind, int space, const dou
   if (int r = check_ctx(ctx)) return r;
   if (int r = check_batch(ctx, kind, space, P, B)) return r;
   return launch(ctx, kind, space, d_theta, P, B, d_T_use, d_out, nullptr, nullptr, s, 0, 0, nullptr, true, ws);
+}
+
+void set_lane_share(yfm_ctx* ctx, int share) {
+  if (ctx) ctx->lane_share = share > 1 ? share : 1;
 }
 
 }  // namespace yfm

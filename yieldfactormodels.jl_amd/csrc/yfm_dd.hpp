@@ -197,6 +197,18 @@ __device__ __forceinline__ dd dd_exp(dd x) {
   return dd_ldexp(e, (int)k);
 }
 
+// x^n, n ≥ 0, by binary powering: ⌈log2 n⌉ squarings and popcount(n) products, relative error ≲ (2 log2 n + 2)·4u²
+// on top of n times x's own (the TVλ dd filter's e^{−λkΔ} = (e^{−λΔ})^k on integer maturity grids)
+__device__ __forceinline__ dd dd_powi(dd x, int n) {
+  dd r = dd_make(1.0);
+  while (n > 0) {  // data-dependent trip count (≤ 9 for n < 512)
+    if (n & 1) r = dd_mul(r, x);
+    n >>= 1;
+    if (n) x = dd_mul(x, x);
+  }
+  return r;
+}
+
 // ---- shared by the double-double filters (yfm_tvl_dd.hip, yfm_fixedz_dd.hip) ----
 
 // −λ·m in dd for exp(−λm); a product that overflows (λ near the FP64 range) is −Inf, whose exp is

@@ -312,6 +312,12 @@ extern "C" int yfm_estimate(yfm_ctx* ctx, int model_kind, int param_space, const
       for (yfm::Workspace* x : w) yfm::workspace_destroy(x);
     }
   } release{sts, wss, d_th, d_out, d_tu};
+  // the G groups' launches run side by side: each group's TVλ launch is sized for its share of the device
+  struct Share {
+    yfm_ctx* c;
+    ~Share() { yfm::set_lane_share(c, 1); }
+  } share_reset{ctx};
+  yfm::set_lane_share(ctx, G);
   for (int g = 0; g < G; ++g)
     if (hipStreamCreateWithFlags(&sts[g], hipStreamNonBlocking) != hipSuccess)
       return yfm::api_error(YFM_EHIP, "stream creation failed for the estimation batch");

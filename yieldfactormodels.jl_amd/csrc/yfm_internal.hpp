@@ -44,19 +44,28 @@ hipError_t launch_fixedz_group(int kind, const LaunchArgs& a);
 // (yfm_fixedz_dd.hip): per-candidate dd records of fixedz_dd_scratch_bytes(kind, B) bytes
 size_t fixedz_dd_scratch_bytes(int kind, int B);
 hipError_t launch_fixedz_dd(int kind, const LaunchArgs& a, double* rec);
-// TVλ EKF kernel (yfm_tvl.hip): lanes per filter for a batch, largest N, launcher
-int tvl_lanes_for(int B, int N);
+// TVλ EKF kernel (yfm_tvl.hip): lanes per filter for a batch, largest N, launcher.  `share`: launches of this
+// size the caller runs concurrently on the device (the estimation driver's chain groups; 1 otherwise)
+int tvl_lanes_for(int B, int N, int share = 1);
 int tvl_max_n();
 size_t tvl_scratch_bytes(int B);
 // Maturity jump table for the TVλ exp recurrence (built on the host per lane count L):
 // the distinct values d_k of m_{i+L} − m_i and, per maturity i, the index k of its jump.
 // K = 0 disables the recurrence (one exp per maturity).
+// Power mode (the certified kernel, when the jumps are too many or inexact): every maturity is an exact integer
+// multiple k_i·Δ of one step Δ (integer-month grids), so e^{−λm_i} = b^{k_i} with b = e^{−λΔ} — one dd exp per
+// step and integer powers of b for the lane starts and the Kp ≤ kTvlPowGaps distinct jump exponents e_q.
 constexpr int kTvlGaps = 8;
+constexpr int kTvlPowGaps = 16;
 struct TvlGaps {
   int K = 0;
   bool exact = false;         // every jump is the exact difference of its two maturities
   const double* d = nullptr;  // device, kTvlGaps
   const int* idx = nullptr;   // device, N
+  int Kp = 0;                 // power mode: distinct jump exponents (0: not available)
+  double step = 0.0;          // Δ
+  const double* e = nullptr;  // device, kTvlPowGaps: the exponents e_q (integers, as doubles)
+  const int* pidx = nullptr;  // device, N: each maturity's jump index q
 };
 hipError_t launch_tvl(const LaunchArgs& a, const TvlGaps& g, int lanes);
 // per-candidate FP64 record of the TVλ init kernel (decoded θ + initial state), doubles
@@ -65,9 +74,9 @@ constexpr int kRecLen = 48;  // padded to 16-byte multiples
 // the same filter in double-double arithmetic (yfm_tvl_dd.hip), YFM_PREC_CERTIFIED: the init
 // kernel writes the per-candidate dd records and the panel's dd column sums into `rec_dd`
 // (tvl_dd_scratch_bytes(B, T));
-// tvl_dd_lanes_for picks the lanes per filter (`want` > 0: a requested width, clamped)
+// tvl_dd_lanes_for picks the lanes per filter (`want` > 0: a requested width, clamped; `share` as tvl_lanes_for)
 size_t tvl_dd_scratch_bytes(int B, int T);
-int tvl_dd_lanes_for(int B, int N, int want);
+int tvl_dd_lanes_for(int B, int N, int want, int share = 1);
 hipError_t launch_tvl_dd_init(const LaunchArgs& a, double* rec_dd);
 hipError_t launch_tvl_dd(const LaunchArgs& a, const double* rec_dd, const TvlGaps& g, int lanes);
 // Trajectory outputs (yfm_predict.hip) from a recorded state trajectory.
@@ -99,6 +108,9 @@ Workspace* workspace_create();
 void workspace_destroy(Workspace* w);
 int loglik_device_ws(yfm_ctx* ctx, Workspace* ws, int kind, int space, const double* d_theta, int P, int B,
                      const int* d_T_use, double* d_out, hipStream_t s);
+// concurrent launches of similar size the caller keeps in flight (the TVλ lane choice sizes the device's share of
+// each launch by it); the estimation driver sets its chain-group count and restores 1
+void set_lane_share(yfm_ctx* ctx, int share);
 // record `msg` as yfm_last_error() for this thread and return `code` (host helpers above the C ABI)
 int api_error(int code, const char* msg);
 // columns of the context's panel (0 before yfm_set_panel)

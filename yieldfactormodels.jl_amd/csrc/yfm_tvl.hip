@@ -558,17 +558,30 @@ size_t tvl_scratch_bytes(int B) { return sizeof(double) * (size_t)kRecLen * (siz
 
 int tvl_max_n() { return (kTvlPre * kTvlBlock) - 1; }
 
-int tvl_lanes_for(int B, int N) {
-  // enough lanes for two waves per SIMD (256 CUs × 4 SIMDs × 2 × 64 lanes — the kernel is built
-  // for two), capped at a wave and at the maturity count rounded up to a power of two.  Measured
-  // on MI355X at N = 360, steady clock (profiles/r1/final/tvl_lanes): B = 16,384 → L = 8 takes
-  // 5.77 ms vs 6.06 ms at L = 4 and 7.65 ms at L = 16; B = 65,536 → L = 2.
-  long long want = (2048LL * 64 + B - 1) / (B > 0 ? B : 1);
-  int L = 1;
-  while (L < want && L < 64) L <<= 1;
+int tvl_lanes_for(int B, int N, int share) {
+  // The L (a power of two ≤ 64, ≤ the maturity count rounded up) with the least modelled time.  Per filter step a
+  // wave issues ≈ ⌈N/L⌉·28 instructions of maturity loop, ≈ 1,450 of 4×4 update and per-step constants (replicated
+  // on every lane of a group) and ≈ 60 per butterfly level; the kernel holds two waves per SIMD (2,048 on the chip)
+  // and issues at ≈ 0.7 of that rate with one (L = 4 vs 8 at B = 16,384, N = 360: 6.06 vs 5.77 ms,
+  // profiles/r1/final/tvl_lanes).  `share` concurrent launches of this size divide the SIMDs.  Measured choices it
+  // keeps at N = 360: B = 16,384 → 8, B = 65,536 → 2, B ≤ 1,024 → 64.  At N = 30 the update dominates: the
+  // estimator's 7,680-point rounds take L = 4 (the round-4 rule, "fill two waves per SIMD", gave 32).
   int capN = 1;
   while (capN < N && capN < 64) capN <<= 1;
-  return L < capN ? L : capN;
+  const double waves_per_simd_unit = (double)(B > 0 ? B : 1) * (share > 0 ? share : 1) / (64.0 * 1024.0);
+  int best = 1;
+  double best_cost = 0.0;
+  for (int L = 1, lg = 0; L <= capN; L <<= 1, ++lg) {
+    const double wps = waves_per_simd_unit * L;  // waves per SIMD
+    const double issue = (double)((N + L - 1) / L) * 28.0 + 1450.0 + 60.0 * lg;
+    const double eff = wps >= 2.0 ? 1.0 : (wps <= 1.0 ? 0.7 : 0.7 + 0.3 * (wps - 1.0));
+    const double cost = (wps > 1.0 ? wps : 1.0) * issue / eff;
+    if (L == 1 || cost < best_cost) {
+      best = L;
+      best_cost = cost;
+    }
+  }
+  return best;
 }
 
 hipError_t launch_tvl(const LaunchArgs& a, const TvlGaps& g, int lanes) {

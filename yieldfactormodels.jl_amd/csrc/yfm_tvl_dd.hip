@@ -38,9 +38,10 @@ namespace {
 constexpr int kDdBlock = 256;
 constexpr int kDdPre = 8;  // panel doubles prefetched per thread per chunk
 constexpr int M4 = 4;
-// per-group jump factors e^{−λ d_k} in LDS: 9 dd (144 B) apart, so the 16 groups of a wave
-// reading their own table hit disjoint banks (a 128 B stride is a 4-way conflict)
-constexpr int kDdWStride = kTvlGaps + 1;
+// per-group jump factors e^{−λ d_k} in LDS: 17 dd (272 B) apart, so the 16 groups of a wave
+// reading their own table hit disjoint banks (a power-of-two stride is a 4-way conflict)
+constexpr int kDdJumps = kTvlPowGaps > kTvlGaps ? kTvlPowGaps : kTvlGaps;
+constexpr int kDdWStride = kDdJumps + 1;
 
 // per-candidate record written by tvl_dd_init_kernel (doubles)
 constexpr int kDSig = 0;     // σ² (dd)
@@ -295,8 +296,9 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
     const double* __restrict__ rec, int B, const double* __restrict__ Y, const double* __restrict__ colsum,
     const double* __restrict__ prep, int ldp,
     int np, int T, int N, int TC, const double* __restrict__ mats, int K, const double* __restrict__ gap_d,
-    const int* __restrict__ gap_idx, const int* __restrict__ T_use, double* __restrict__ out, unsigned int* __restrict__ flags, double* __restrict__ rec_beta,
-    double* __restrict__ rec_P, int horizon, int rec_len) {
+    const int* __restrict__ gap_idx, double pstep, const int* __restrict__ T_use, double* __restrict__ out,
+    unsigned int* __restrict__ flags, double* __restrict__ rec_beta, double* __restrict__ rec_P, int horizon,
+    int rec_len) {
   constexpr int GPB = kDdBlock / L;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   constexpr int kSumDd = 2;                            // dd column sums per staged column
@@ -310,8 +312,9 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
   dd* s_w = reinterpret_cast<dd*>(s_par + GPB * kDPar);  // per group: e^{-λ d_k}, k < K
   dd* s_xch = s_w + GPB * kDdWStride;                  // per group: 4×4 dd exchange block
   int* s_gi = reinterpret_cast<int*>(s_xch + GPB * M4 * M4);
-  __shared__ double s_gd[kTvlGaps];
-  __shared__ int s_gsrc[kTvlGaps];  // a lane whose first maturity equals jump k exactly, or −1
+  // jump k: the maturity difference d_k, or (power mode, pstep = Δ > 0) its exponent e_k: e^{−λd_k} = (e^{−λΔ})^{e_k}
+  __shared__ double s_gd[kDdJumps];
+  __shared__ int s_gsrc[kDdJumps];  // a lane whose first maturity equals jump k exactly, or −1
   __shared__ int s_nobs_max;
 
   const int tid = threadIdx.x;
@@ -333,7 +336,8 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
     const double d = gap_d[tid];
     s_gd[tid] = d;
     int src = -1;
-    for (int q = min(L, N) - 1; q >= 0; --q) src = mats[q] == d ? q : src;
+    if (pstep == 0.0)
+      for (int q = min(L, N) - 1; q >= 0; --q) src = mats[q] == d ? q : src;
     s_gsrc[tid] = src;
   }
   const double* r = rec + (size_t)bb * kDRecLen;
@@ -472,10 +476,7 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
       const double sgzz = split_const(l_n * Be * Be);
       const double sy2 = split_const(By * Bz2), syz = split_const(By * Be);
       dd_acc S2, Sz, S4, G22, G2z, G24, Gzz, Gz4, G44, Y2, Yz, Y4;
-      auto accum = [&](int i, dd z) {
-        const double m = s_m[i];
-        const double y = col[i];
-        const dd rm = s_rm[i];
+      auto accum = [&](double m, double y, dd rm, dd z) {
         const dd it = dd_mul_nn(rl, rm);  // 1/τ
         // 1 − z exactly (Fast2Sum: 1 ≥ z.hi), then (1 − z)/τ
         const double o1 = 1.0 - z.hi;
@@ -508,23 +509,61 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
       };
       if (K > 0) {
         dd* w = s_w + grp * kDdWStride;
-        dd z = (j < N) ? dd_exp(neg_rate(lam, s_m[j])) : dd_make(0.0);
-        // a jump equal to some lane's first maturity (uniform grids: d = L·Δ = m_{L−1}) is that
-        // lane's start value — the same dd_exp of the same argument — so only the others cost an exp
-        for (int q = 0; q < K; ++q)
-          if (s_gsrc[q] == j) w[q] = z;
-        for (int q = j; q < K; q += L)
-          if (s_gsrc[q] < 0) w[q] = dd_exp(neg_rate(lam, s_gd[q]));
+        dd z;
+        if (pstep > 0.0) {
+          // power mode: one dd exp, b = e^{−λΔ}; the lane's start value and the group's jump factors are integer
+          // powers of it (m_j/Δ and e_q are exact integers) — in place of one dd exp per maturity
+          const dd bs = dd_exp(neg_rate(lam, pstep));
+          z = (j < N) ? dd_powi(bs, (int)(s_m[j] / pstep)) : dd_make(0.0);
+          for (int q = j; q < K; q += L) w[q] = dd_powi(bs, (int)s_gd[q]);
+        } else {
+          z = (j < N) ? dd_exp(neg_rate(lam, s_m[j])) : dd_make(0.0);
+          // a jump equal to some lane's first maturity (uniform grids: d = L·Δ = m_{L−1}) is that
+          // lane's start value — the same dd_exp of the same argument — so only the others cost an exp
+          for (int q = 0; q < K; ++q)
+            if (s_gsrc[q] == j) w[q] = z;
+          for (int q = j; q < K; q += L)
+            if (s_gsrc[q] < 0) w[q] = dd_exp(neg_rate(lam, s_gd[q]));
+        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (int i = j; i < N; i += L) {
-          const dd wn = w[s_gi[i]];
-          accum(i, z);
-          z = dd_mul(z, wn);
+        // the LDS operands of maturity i + L are read while maturity i is accumulated (at one wave per SIMD a
+        // read at the top of the iteration it feeds stalls the wave for the LDS latency); the last read is a
+        // harmless repeat of maturity N − 1
+        const int last = N - 1;
+        const int i0 = min(j, last);
+        double m_n = s_m[i0], y_n = col[i0];
+        dd rm_n = s_rm[i0];
+        if (K == 1) {
+          // one jump (uniform grids): the factor is loop-invariant
+          const dd wn = w[0];
+          for (int i = j; i < N; i += L) {
+            const double m = m_n, y = y_n;
+            const dd rm = rm_n;
+            const int in = min(i + L, last);
+            m_n = s_m[in];
+            y_n = col[in];
+            rm_n = s_rm[in];
+            accum(m, y, rm, z);
+            z = dd_mul(z, wn);
+          }
+        } else {
+          dd wn_n = w[s_gi[i0]];
+          for (int i = j; i < N; i += L) {
+            const double m = m_n, y = y_n;
+            const dd rm = rm_n, wn = wn_n;
+            const int in = min(i + L, last);
+            m_n = s_m[in];
+            y_n = col[in];
+            rm_n = s_rm[in];
+            wn_n = w[s_gi[in]];
+            accum(m, y, rm, z);
+            z = dd_mul(z, wn);
+          }
         }
       } else {
-        for (int i = j; i < N; i += L) accum(i, dd_exp(neg_rate(lam, s_m[i])));
+        for (int i = j; i < N; i += L) accum(s_m[i], col[i], s_rm[i], dd_exp(neg_rate(lam, s_m[i])));
       }
       const dd s2 = group_sum_acc<L>(S2), sz = group_sum_acc<L>(Sz), s4 = group_sum_acc<L>(S4);
       const dd g22 = group_sum_acc<L>(G22), g2z = group_sum_acc<L>(G2z), g24 = group_sum_acc<L>(G24);
@@ -702,10 +741,12 @@ hipError_t launch_tvl_dd_l(const LaunchArgs& a, const double* rec_dd, const TvlG
     if (e != hipSuccess) return e;
   }
   const double* colsum = rec_dd + (size_t)kDRecLen * (size_t)(a.B > 0 ? a.B : 1);
+  // the exact jump table if there is one, else the power mode if the grid allows it, else one exp per maturity
+  const bool pw = g.K == 0 && g.Kp > 0;
   hipLaunchKernelGGL(k, dim3(grid), dim3(kDdBlock), shmem, a.stream, rec_dd, a.B, a.raw, colsum, a.panel, a.ldp,
-                     a.np, a.T,
-                     a.N, TC, a.mats, g.K, g.d, g.idx, a.T_use, a.out, a.flags, a.rec_beta, a.rec_P,
-                     a.rec_beta ? a.horizon : 0, a.rec_beta ? a.rec_len : 0);
+                     a.np, a.T, a.N, TC, a.mats, pw ? g.Kp : g.K, pw ? g.e : g.d, pw ? g.pidx : g.idx,
+                     pw ? g.step : 0.0, a.T_use, a.out, a.flags, a.rec_beta, a.rec_P, a.rec_beta ? a.horizon : 0,
+                     a.rec_beta ? a.rec_len : 0);
   return hipGetLastError();
 }
 
@@ -716,21 +757,37 @@ size_t tvl_dd_scratch_bytes(int B, int T) {
   return sizeof(double) * ((size_t)kDRecLen * (size_t)(B > 0 ? B : 1) + 5 * (size_t)(T > 0 ? T : 1));
 }
 
-int tvl_dd_lanes_for(int B, int N, int want) {
-  // one wave per SIMD of lanes (the kernel needs the whole 512-register file per lane), at
-  // least 4 lanes per filter (the per-group parameter block of 256 / L groups must fit the
-  // 64 KiB of dynamic LDS a launch gets by default), capped at the maturity count
-  int L = 1;
+int tvl_dd_lanes_for(int B, int N, int want, int share) {
+  // at least 4 lanes per filter (the 4×4 update is distributed over a lane quad, and the per-group parameter block
+  // of 256 / L groups must fit the 64 KiB of dynamic LDS a launch gets by default), at most 64 and the maturity
+  // count rounded up
+  int capN = 4;
+  while (capN < N && capN < 64) capN <<= 1;
   if (want > 0) {
+    int L = 4;
     while (L < want && L < 64) L <<= 1;
-  } else {
-    const long long lanes = (1024LL * 64 + B - 1) / (B > 0 ? B : 1);
-    while (L < lanes && L < 64) L <<= 1;
-    int capN = 1;
-    while (capN < N && capN < 64) capN <<= 1;
-    L = L < capN ? L : capN;
+    return L;
   }
-  return L < 4 ? 4 : L;
+  // The L with the least modelled time.  The kernel needs the whole register file (one wave per SIMD, 1,024 on the
+  // chip), so waves run in rounds of 1,024; per filter step a wave issues ≈ ⌈N/L⌉·137 instructions of maturity loop,
+  // ≈ 4,250 of 4×4 dd update and per-step constants (replicated on every quad of a group) and ≈ 200 per butterfly
+  // level (instruction counts of this build's ISA).  `share` concurrent launches of this size divide the SIMDs.
+  // Measured choices it keeps at N = 360: B = 16,384 → 4, B ≤ 1,024 → 64 (profiles/r5/first/c3_B*_L*.json).  At
+  // N = 30 the update dominates: the estimator's 7,680-point rounds (two at once) take L = 4, where the round-5
+  // rule ("one wave per SIMD of lanes") gave 16 — four rounds of waves instead of one.
+  const double waves_unit = (double)(B > 0 ? B : 1) * (share > 0 ? share : 1) / 64.0;
+  int best = 4;
+  double best_cost = 0.0;
+  for (int L = 4, lg = 2; L <= capN; L <<= 1, ++lg) {
+    const double rounds = std::ceil(waves_unit * L / 1024.0);
+    const double issue = (double)((N + L - 1) / L) * 137.0 + 4250.0 + 200.0 * lg;
+    const double cost = rounds * issue;
+    if (L == 4 || cost < best_cost) {
+      best = L;
+      best_cost = cost;
+    }
+  }
+  return best;
 }
 
 hipError_t launch_tvl_dd_init(const LaunchArgs& a, double* rec_dd) {
