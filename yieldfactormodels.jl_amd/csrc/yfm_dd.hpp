@@ -298,7 +298,10 @@ __device__ __forceinline__ dd dd_from_R_to_11(double x) {
 
 // Sum of an unnormalised dd over the aligned group of L lanes: each butterfly level pairs
 // every lane with its partner and both form the same exact-leading-part sum, so all lanes
-// of the group end with bitwise the same value.
+// of the group end with bitwise the same value.  The pair needs no canonical order: FP addition
+// is commutative and TwoSum's error term is the exact a + b − fl(a + b) whichever operand comes
+// first, so (own, partner) and (partner, own) give the same bits (round 6: the lane-order selects,
+// 8 v_cndmask per value and level, are gone; logliks bitwise unchanged).
 template <int LVL>
 __device__ __forceinline__ void pair_exchange(double x, double& a, double& b) {
   const int lo = __double2loint(x), hi = __double2hiint(x);
@@ -306,12 +309,8 @@ __device__ __forceinline__ void pair_exchange(double x, double& a, double& b) {
     constexpr int ctrl = LVL == 0 ? 0xB1 : LVL == 1 ? 0x4E : LVL == 2 ? 0x141 : 0x140;
     const int plo = __builtin_amdgcn_mov_dpp(lo, ctrl, 0xf, 0xf, true);
     const int phi = __builtin_amdgcn_mov_dpp(hi, ctrl, 0xf, 0xf, true);
-    const double p = __hiloint2double(phi, plo);
-    // canonical order (lower lane's value first) so both partners compute the same bits
-    const bool lower = LVL == 0 ? !(threadIdx.x & 1) : LVL == 1 ? !(threadIdx.x & 2)
-                     : LVL == 2 ? !(threadIdx.x & 4) : !(threadIdx.x & 8);
-    a = lower ? x : p;
-    b = lower ? p : x;
+    a = x;
+    b = __hiloint2double(phi, plo);
   } else if constexpr (LVL == 4) {
     const auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
     const auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);

@@ -42,6 +42,9 @@ constexpr int M4 = 4;
 // reading their own table hit disjoint banks (a power-of-two stride is a 4-way conflict)
 constexpr int kDdJumps = kTvlPowGaps > kTvlGaps ? kTvlPowGaps : kTvlGaps;
 constexpr int kDdWStride = kDdJumps + 1;
+// per-group 4×4 dd exchange blocks 17 dd (272 B) apart: at 16 dd (256 B = 64 banks) the 16 groups of a wave
+// exchanging the same entry all hit the same banks — a 16-way conflict on every transpose
+constexpr int kXchStride = 4 * 4 + 1;
 
 // per-candidate record written by tvl_dd_init_kernel (doubles)
 constexpr int kDSig = 0;     // σ² (dd)
@@ -311,7 +314,7 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
   double* s_par = s_y + TC * N;                        // per group: σ², δ, Φ, Q (kDPar doubles)
   dd* s_w = reinterpret_cast<dd*>(s_par + GPB * kDPar);  // per group: e^{-λ d_k}, k < K
   dd* s_xch = s_w + GPB * kDdWStride;                  // per group: 4×4 dd exchange block
-  int* s_gi = reinterpret_cast<int*>(s_xch + GPB * M4 * M4);
+  int* s_gi = reinterpret_cast<int*>(s_xch + GPB * kXchStride);
   // jump k: the maturity difference d_k, or (power mode, pstep = Δ > 0) its exponent e_k: e^{−λd_k} = (e^{−λΔ})^{e_k}
   __shared__ double s_gd[kDdJumps];
   __shared__ int s_gsrc[kDdJumps];  // a lane whose first maturity equals jump k exactly, or −1
@@ -358,7 +361,7 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
 
   // the 4×4 update is distributed over the lanes of each quad: role qr holds column qr of P
   const int qr = tid & 3;
-  dd* xch = s_xch + grp * M4 * M4;
+  dd* xch = s_xch + grp * kXchStride;
   dd beta[M4], Pc[M4];
 #pragma unroll
   for (int i = 0; i < M4; ++i) {
@@ -731,7 +734,7 @@ hipError_t launch_tvl_dd_l(const LaunchArgs& a, const double* rec_dd, const TvlG
   // the kernel's LDS layout: m, 1/m, per staged column NaN flag, dd sums, max|y| and N yields, per group the
   // parameters, jump factors and exchange block, and the jump index per maturity
   const size_t shmem = sizeof(double) * (size_t)(3 * a.N + (2 + 2 * kSumDd) * TC + TC * a.N + GPB * kDPar +
-                                                 2 * GPB * kDdWStride + 2 * GPB * M4 * M4) +
+                                                 2 * GPB * kDdWStride + 2 * GPB * kXchStride) +
                        sizeof(int) * a.N;
   if (shmem > 160 * 1024) return hipErrorInvalidValue;  // gfx950: 160 KiB of LDS per workgroup
   auto* k = a.rec_beta ? &tvl_dd_loglik_kernel<L, true> : &tvl_dd_loglik_kernel<L, false>;
