@@ -94,6 +94,10 @@ def run(kind, Y, mats, Thc, rule=None, tau=2.0 ** -50):
     N, T = Y.shape
     Z = loadings(g, mats)
     G = np.einsum("bni,bnj->bij", Z, Z)
+    # candidates whose Z'Z is ill-conditioned go to the kernel's double-double path, not the collapsed filter
+    # modelled here (κ₁ ≥ 1e6, yfm_fixedz.hpp): their G is replaced by I and their results are NaN
+    bad = ~(np.linalg.cond(G, 1) < 1e6)
+    G = np.where(bad[:, None, None], np.eye(G.shape[1])[None], G)
     Gi = np.linalg.inv(G)
     R = s2[:, None, None] * Gi
     R = 0.5 * (R + np.swapaxes(R, 1, 2))
@@ -155,6 +159,7 @@ def run(kind, Y, mats, Thc, rule=None, tau=2.0 ** -50):
     nterms = T - 2
     per = (N - M) * np.log(s2) + ldG + N * LOG2PI
     ll = -0.5 * (nterms * per + ld + sq)
+    ll = np.where(bad, np.nan, ll)  # deferred to the double-double kernel
     return ll, fstep, drift_bound, sens
 
 
