@@ -71,6 +71,25 @@ def test_bench_self_launches_n_ranks():
     assert line["config"]["global_batch"] == 2 * 4096 and "spawn_local_ranks" in line["launcher"]
 
 
+@pytest.mark.parametrize("config", [4, 5])
+def test_bench_emulate_world(config):
+    """`bench.py --emulate-world 4` (the one-GPU prediction of the strong-scaled configurations' N-GPU
+    efficiency): every rank's shard is timed, the shards are the ranks' own (their batches add up to the whole
+    job), and the prediction is T₁ / (W · max_R T_R), a number in (0, 1.2]."""
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--config", str(config), "--batch", "512" if config == 4 else "65536",
+           "--T", "120", "--emulate-world", "4", "--steps", "3", "--warmup", "1", "--settle-seconds", "0"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=str(ROOT))
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    print({k: line[k] for k in ("predicted_efficiency", "max_rank_kernel_ms", "rank_imbalance")})
+    assert sorted(line["ranks"]) == ["0", "1", "2", "3"]
+    assert sum(s["batch"] for s in line["ranks"].values()) == line["world1"]["batch"]
+    assert sum(s["filter_steps"] for s in line["ranks"].values()) == line["world1"]["filter_steps"]
+    t1, tmax = line["world1"]["kernel_ms_mean"], line["max_rank_kernel_ms"]
+    assert abs(line["predicted_efficiency"] - t1 / (4 * tmax)) < 1e-12
+    assert 0.0 < line["predicted_efficiency"] <= 1.2
+
+
 def _rolling_worker(rank, world, port, Y, mats, out_dir, ret):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch  # noqa: F401
