@@ -166,6 +166,8 @@ def main():
     ap.add_argument("--max-group-iters", type=int, default=10)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-cpu-opt", action="store_true")
+    ap.add_argument("--precision", choices=["certified", "fp64"], default="certified",
+                    help="TVλ arithmetic of the GPU leg (the library default is certified; fp64 is the reference's class)")
     args = ap.parse_args()
     kind = KIND_TVL if args.model == "tvl" else KIND_DNS
     mats = S.maturities_30() if args.N == 30 else S.maturities_360()
@@ -177,13 +179,15 @@ def main():
     cpu_opt = None if args.no_cpu_opt else cpu_optimised_leg(kind, Y, mats, wins, th0, args)
     torch.cuda.set_device(0)
     eng = Engine(0)
+    from yfm_amd import _lib
+    eng.precision = _lib.PREC_FP64 if args.precision == "fp64" else _lib.PREC_CERTIFIED
     eng.set_panel(Y, mats)
     Th0 = np.repeat(th0[:, None], len(wins), axis=1)
     eng.estimate(kind, Th0[:, :2], space=1, T_use=wins[:2], iterations=5, max_group_iters=1)  # warm up
     t0 = time.perf_counter()
     r = eng.estimate(kind, Th0, space=1, T_use=wins, iterations=args.iterations, max_group_iters=args.max_group_iters)
     gpu_s = time.perf_counter() - t0
-    name = "TVλ EKF (certified)" if kind == KIND_TVL else "DNS"
+    name = f"TVλ EKF ({args.precision})" if kind == KIND_TVL else "DNS"
     out = {"metric": f"rolling re-estimation (estimate_steps!, NelderMead opt1), {name} T≤600 N={len(mats)}",
            "windows": int(len(wins)), "iterations": args.iterations, "max_group_iters": args.max_group_iters,
            "gpu_seconds_all_windows": gpu_s, "gpu_seconds_per_task": gpu_s / len(wins),
