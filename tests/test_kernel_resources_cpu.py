@@ -21,6 +21,8 @@ BUDGETS = {
     "fixedz_loglik_kernelILi30ELi3ELi1ELb0ELb0ELb0EE": 0,
     # config 5: GNS5, NP = 30, full recursion
     "fixedz_loglik_kernelILi30ELi5ELi2ELb0ELb0ELb0EE": 0,
+    # config 5: the GNS5 initial state, two lanes per candidate (the per-lane kernel spills 540 B/lane)
+    "fixedz_init_coop_kernelILi5ELi2ELi2E": 0,
     # config 3: certified TVλ at L = 4
     "tvl_dd_loglik_kernelILi4ELb0E": 0,
 }

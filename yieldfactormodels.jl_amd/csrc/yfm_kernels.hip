@@ -98,6 +98,157 @@ __global__ __launch_bounds__(256) void fixedz_init_kernel(const double* __restri
   rec[(size_t)q * B + b] = ok ? 1.0 : 0.0;
 }
 
+// The value of role O of this lane's aligned group of R lanes (R = 2: lane pairs, 4: quads): DPP quad_perm.
+template <int R, int O>
+__device__ __forceinline__ double role_bcast(double x) {
+  static_assert(R == 2 || R == 4, "groups inside one quad");
+  constexpr int ctrl = R == 4 ? (O | (O << 2) | (O << 4) | (O << 6)) : (O | (O << 2) | ((2 + O) << 4) | ((2 + O) << 6));
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), ctrl, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), ctrl, 0xf, 0xf, true);
+  return __hiloint2double(hi, lo);
+}
+template <int R>
+__device__ __forceinline__ double role_bcast_from(int o, double x) {  // o constant after unrolling
+  if constexpr (R == 2) {
+    return o == 0 ? role_bcast<2, 0>(x) : role_bcast<2, 1>(x);
+  } else {
+    return o == 0 ? role_bcast<4, 0>(x) : o == 1 ? role_bcast<4, 1>(x) : o == 2 ? role_bcast<4, 2>(x) : role_bcast<4, 3>(x);
+  }
+}
+
+// fixedz_init_kernel with each candidate's Lyapunov system spread over R lanes (GNS5; launched with R = 2).  The per-lane kernel holds
+// the augmented 15×16 system in 480 registers and spills 540 B/lane; here role o of a candidate's R lanes holds the
+// columns c ≡ o (mod R) of [L | q] (16/R columns), so the system fits in registers.  The elimination is gauss_solve's
+// arithmetic, operation for operation: per step every lane receives column k from its owner (DPP), runs the same
+// pivot search on it (identical inputs → the same pivot in every role), exchanges rows k and p in its own columns
+// and updates them with the same multipliers; back substitution runs gauss_solve's FMA chain in every lane with the
+// entries of U broadcast from their owners.  The record is bitwise the per-lane kernel's.  Decoding and β₀ = (I − Φ)\δ
+// are repeated in every role.
+template <int M, int LEAD, int R>
+__global__ __launch_bounds__(256) void fixedz_init_coop_kernel(const double* __restrict__ theta, int P, int B, int space,
+                                                               double* __restrict__ rec,
+                                                               unsigned int* __restrict__ flags_next) {
+  if (flags_next && blockIdx.x == 0 && threadIdx.x < kFlagsPerBank) flags_next[threadIdx.x] = 0u;  // the next launch's counters
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = g / R;
+  const int role = threadIdx.x & (R - 1);
+  if (b >= B) return;  // B·R threads round up to whole groups: a group is live or not as a whole
+  Params<M, LEAD> p;
+  decode_params<M, LEAD>(theta + (size_t)b * P, space, p);
+  double beta[M];
+  bool ok;
+  {
+    double A[M][M], x[M][1];
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+#pragma unroll
+      for (int j = 0; j < M; ++j) A[i][j] = (i == j ? 1.0 : 0.0) - p.Phi[i][j];
+      x[i][0] = p.delta[i];
+    }
+    ok = gauss_solve<M, 1>(A, x);
+#pragma unroll
+    for (int i = 0; i < M; ++i) beta[i] = x[i][0];
+  }
+  constexpr int S = M * (M + 1) / 2;     // unknowns P_kl, k ≤ l
+  constexpr int NS = (S + 1 + R - 1) / R;  // local columns (the right-hand side is global column S)
+  double a[NS][S];
+  // build: row (i, j), column (k, l) of I − (the symmetric-subspace restriction of Φ⊗Φ), exactly init_state's;
+  // column by column, each lane keeping its own (global column c → local column c / R of role c % R)
+  {
+    auto put = [&](int c, int r, double v) {
+      if (c % R == 0) {
+        a[c / R][r] = v;
+      } else {
+        a[c / R][r] = role == c % R ? v : a[c / R][r];
+      }
+    };
+    int c = 0;
+#pragma unroll
+    for (int k = 0; k < M; ++k)
+#pragma unroll
+      for (int l = k; l < M; ++l, ++c) {
+        int r = 0;
+#pragma unroll
+        for (int i = 0; i < M; ++i)
+#pragma unroll
+          for (int j = i; j < M; ++j, ++r) {
+            double s = p.Phi[i][k] * p.Phi[j][l];
+            if (k != l) s = fma(p.Phi[i][l], p.Phi[j][k], s);
+            put(c, r, (r == c ? 1.0 : 0.0) - s);
+          }
+      }
+    int r = 0;
+#pragma unroll
+    for (int i = 0; i < M; ++i)
+#pragma unroll
+      for (int j = i; j < M; ++j, ++r) {
+        put(S, r, p.Q[i][j]);
+#pragma unroll
+        for (int c2 = S + 1; c2 < NS * R; ++c2) put(c2, r, 0.0);
+      }
+  }
+  // elimination with partial pivoting (gauss_solve's pivot rule and arithmetic)
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+    const int o = k % R, sk = k / R;
+    double col[S];
+#pragma unroll
+    for (int i = k; i < S; ++i) col[i] = role_bcast_from<R>(o, a[sk][i]);
+    int pv = k;
+    double amax = fabs(col[k]);
+#pragma unroll
+    for (int i = k + 1; i < S; ++i) {
+      const double v = fabs(col[i]);
+      const bool gt = v > amax;
+      amax = gt ? v : amax;
+      pv = gt ? i : pv;
+    }
+#pragma unroll
+    for (int i = k + 1; i < S; ++i) {
+      const bool sw = pv == i;
+      const double ck = col[k], ci = col[i];
+      col[k] = sw ? ci : ck;
+      col[i] = sw ? ck : ci;
+      // local columns below sk hold eliminated columns only; in slot sk the roles whose column is ≤ k exchange
+      // and update entries below the diagonal that are never read again
+#pragma unroll
+      for (int s = sk; s < NS; ++s) {
+        const double u = a[s][k], w = a[s][i];
+        a[s][k] = sw ? w : u;
+        a[s][i] = sw ? u : w;
+      }
+    }
+    const double piv = col[k];
+    ok = ok && (piv != 0.0);
+    const double rp = 1.0 / piv;
+#pragma unroll
+    for (int i = k + 1; i < S; ++i) {
+      const double l = col[i] * rp;
+#pragma unroll
+      for (int s = sk; s < NS; ++s) a[s][i] = fma(-l, a[s][k], a[s][i]);
+    }
+  }
+  // back substitution: x_k = (q_k − Σ_{j>k} U_kj x_j) / U_kk in gauss_solve's order.  The running sum travels:
+  // every lane applies its own column's entry and the result of the owner of column j is taken (x is replicated),
+  // so no entry of U is copied out of its owner and each hop depends on the last
+  double x[S];
+#pragma unroll
+  for (int k = S - 1; k >= 0; --k) {
+    const double rp = role_bcast_from<R>(k % R, 1.0 / a[k / R][k]);
+    double s = role_bcast_from<R>(S % R, a[S / R][k]);
+#pragma unroll
+    for (int j = k + 1; j < S; ++j) s = role_bcast_from<R>(j % R, fma(-a[j / R][k], x[j], s));
+    x[k] = s * rp;
+  }
+  if (role != 0) return;
+  int q = 0;
+#pragma unroll
+  for (int i = 0; i < M; ++i) rec[(size_t)(q++) * B + b] = beta[i];
+#pragma unroll
+  for (int r = 0; r < S; ++r) rec[(size_t)(q++) * B + b] = x[r];
+  rec[(size_t)q * B + b] = ok ? 1.0 : 0.0;
+}
+
 // ---- per-step building blocks (all __forceinline__: the fast path is one basic block) ----
 
 // z̃ = Z'ỹ_t for the NZ non-constant loading columns (Σỹ = 0 removes column 0).
@@ -853,13 +1004,29 @@ static int split_form_enabled() {
   return (e && e[0] == '1') ? 1 : 0;
 }
 
+// GNS5 initial state: two lanes per candidate (fixedz_init_coop_kernel); YFM_GNS5_INIT_LANES=1 runs the per-lane
+// kernel it is bitwise equal to (tests/test_gpu_gns5_init.py).  Four lanes per candidate, at two waves per SIMD,
+// measured slower (0.83 vs 0.74 ms at config 5; per-lane 1.05 ms): the replicated decode and pivot search cost more
+// than the second wave hides (profiles/r6/gns5_init/).
+static int gns5_init_lanes() {
+  const char* e = std::getenv("YFM_GNS5_INIT_LANES");
+  return (e && e[0] == '1' && e[1] == 0) ? 1 : 2;
+}
+
 template <int NP, int M, int LEAD>
 static hipError_t launch_fixedz_np(const LaunchArgs& a) {
   const int grid = (a.B + kBlock - 1) / kBlock;
   if constexpr (M == 5) {
     if (!a.scratch) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((fixedz_init_kernel<M, LEAD>), dim3(grid), dim3(kBlock), 0, a.stream, a.theta, a.P, a.B,
-                       a.space, a.scratch, a.flags_next);
+    const int ir = gns5_init_lanes();
+    if (ir == 1) {
+      hipLaunchKernelGGL((fixedz_init_kernel<M, LEAD>), dim3(grid), dim3(kBlock), 0, a.stream, a.theta, a.P, a.B,
+                         a.space, a.scratch, a.flags_next);
+    } else {
+      const int gi = (int)(((size_t)a.B * 2 + kBlock - 1) / kBlock);
+      hipLaunchKernelGGL((fixedz_init_coop_kernel<M, LEAD, 2>), dim3(gi), dim3(kBlock), 0, a.stream, a.theta, a.P, a.B,
+                         a.space, a.scratch, a.flags_next);
+    }
   }
   if (a.rec_beta) {
     hipLaunchKernelGGL((fixedz_loglik_kernel<NP, M, LEAD, true>), dim3(grid), dim3(kBlock), 0, a.stream, a.theta, a.P,
