@@ -343,13 +343,13 @@ __device__ __forceinline__ dd quad_xor(dd x) {
   constexpr int ctrl = (0 ^ R) | ((1 ^ R) << 2) | ((2 ^ R) << 4) | ((3 ^ R) << 6);
   return {quad_dpp<ctrl>(x.hi), quad_dpp<ctrl>(x.lo)};
 }
-// v[i] for a lane-dependent i in [0, 4)
+// v[i] for a lane-dependent i in [0, 4): a two-level mux on the bits of i (a chain of i == k selects is turned
+// into a scratch-indexed load by the compiler)
 __device__ __forceinline__ dd sel4(const dd (&v)[4], int i) {
-  dd r = v[0];
-  r = i == 1 ? v[1] : r;
-  r = i == 2 ? v[2] : r;
-  r = i == 3 ? v[3] : r;
-  return r;
+  const bool b0 = (i & 1) != 0, b1 = (i & 2) != 0;
+  const dd lo = b0 ? v[1] : v[0];
+  const dd hi = b0 ? v[3] : v[2];
+  return b1 ? hi : lo;
 }
 
 template <int LVL>

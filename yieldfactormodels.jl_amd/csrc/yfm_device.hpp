@@ -506,6 +506,37 @@ __device__ __forceinline__ double quad_bcast_f64(double x) {
   const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), ctrl, 0xf, 0xf, true);
   return __hiloint2double(hi, lo);
 }
+// the value held by role qr ^ R of this lane's quad (R = 1, 2, 3)
+template <int R>
+__device__ __forceinline__ double quad_xor_f64(double x) {
+  constexpr int ctrl = (0 ^ R) | ((1 ^ R) << 2) | ((2 ^ R) << 4) | ((3 ^ R) << 6);
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), ctrl, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), ctrl, 0xf, 0xf, true);
+  return __hiloint2double(hi, lo);
+}
+// v[i] for a lane-dependent i in [0, 4): a two-level mux on the bits of i (a chain of i == k selects is turned
+// into a scratch-indexed load by the compiler)
+__device__ __forceinline__ double sel4_f64(const double (&v)[4], int i) {
+  const bool b0 = (i & 1) != 0, b1 = (i & 2) != 0;
+  const double lo = b0 ? v[1] : v[0];
+  const double hi = b0 ? v[3] : v[2];
+  return b1 ? hi : lo;
+}
+// Column qr of the symmetric 4×4 whose role k holds the upper entries v[i], i ≤ k, of its column: col[k] = v[k] for
+// k ≤ qr and role k's v[qr] below the diagonal — the quad transpose done with DPP alone (role qr ^ d hands over its
+// v[qr] at distance d), no LDS round trip.  The same values as the LDS exchange, bit for bit.
+__device__ __forceinline__ void quad_mirror_f64(int qr, const double (&v)[4], double (&col)[4]) {
+  const double r1 = quad_xor_f64<1>(sel4_f64(v, qr ^ 1));
+  const double r2 = quad_xor_f64<2>(sel4_f64(v, qr ^ 2));
+  const double r3 = quad_xor_f64<3>(sel4_f64(v, qr ^ 3));
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int d = k ^ qr;  // bit mux, as sel4_f64
+    const bool b0 = (d & 1) != 0, b1 = (d & 2) != 0;
+    const double o = b1 ? (b0 ? r3 : r2) : r1;
+    col[k] = k <= qr ? v[k] : o;
+  }
+}
 // rows of a 4×4 whose row S lives in role S, into every lane
 template <int M>
 __device__ __forceinline__ void quad_gather_rows(const double (&row)[M], double (&X)[M][M]) {

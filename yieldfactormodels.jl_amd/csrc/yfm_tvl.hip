@@ -93,8 +93,14 @@ struct TvlQuad {
   double* xch;  // this group's 4×4 exchange block (LDS)
 
   // column qr of the symmetric matrix whose upper entries are `v[i]` for i ≤ qr (this role) and
-  // role k's v[qr] for k > qr
+  // role k's v[qr] for k > qr; DPP: through quad exchanges instead of the LDS block (no wave barriers: the
+  // latency-bound launches, L ≥ 16, take it; the throughput ones keep the fewer instructions of the LDS form)
+  template <bool DPP>
   __device__ __forceinline__ void mirror(const double (&v)[4], double (&col)[4]) const {
+    if constexpr (DPP) {
+      quad_mirror_f64(qr, v, col);
+      return;
+    }
 #pragma unroll
     for (int k = 0; k < 4; ++k) xch[qr * 4 + k] = v[k];
     wave_lds_sync();
@@ -106,6 +112,7 @@ struct TvlQuad {
     wave_lds_sync();  // the block is rewritten by the next exchange
   }
   // β ← δ + Φ bf;  P ← Φ Pf Φ' + Q  (propagate_state, filter.jl:162-176): Pf the full symmetric matrix
+  template <bool DPP>
   __device__ __forceinline__ void propagate(const double (&bf)[4], const double (&Pf)[4][4], double (&beta)[4],
                                             double (&Pc)[4]) const {
     double bq = dq;
@@ -132,7 +139,7 @@ struct TvlQuad {
       for (int l = 0; l < 4; ++l) t = fma(A[i][l], phr[l], t);
       pc[i] = t;
     }
-    mirror(pc, Pc);
+    mirror<DPP>(pc, Pc);
   }
 };
 
@@ -178,6 +185,7 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
   atomicMax(&s_nobs_max, live ? my_steps : 0);
 
   constexpr bool DIST = L >= 4;  // distributed 4×4 update (TvlQuad)
+  constexpr bool XDPP = L >= 16;  // quad transposes by DPP (TvlQuad::mirror)
   Params<M, 0> p;
   double beta[M], Pm[M][M];
   TvlQuad qd;
@@ -272,7 +280,7 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
 #pragma unroll
         for (int i = 0; i < M; ++i) bf[i] = beta[i];
         quad_gather_rows<M>(Pc, Pf);  // P symmetric: role S's column is row S
-        qd.propagate(bf, Pf, beta, Pc);
+        qd.propagate<XDPP>(bf, Pf, beta, Pc);
       } else {
         double bf[M], Pf[M][M];
 #pragma unroll
@@ -333,18 +341,29 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
       if (K > 0) {
         // few distinct jumps d_k = m_{i+L} − m_i: z_{i+L} = z_i · e^{-λ d_k}, one exp per lane
         // plus K per group instead of one per maturity (relative drift ≤ (N/L) ulp)
-        double* w = s_w + grp * kTvlGaps;
-        for (int q = j; q < K; q += L) w[q] = exp(-(lam * s_gd[q]));
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         double z = (j < N) ? exp(-(lam * s_mr[j].x)) : 0.0;
+        if (K == 1) {
+          // one jump (uniform grids): every lane forms the factor itself — the same exp of the same argument,
+          // with no LDS round trip and wave barrier on the step's serial path
+          const double wn = exp(-(lam * s_gd[0]));
 #pragma unroll 2
-        for (int i = j; i < N; i += L) {
-          const double2 mr = s_mr[i];
-          const double wn = w[s_gi[i]];
-          accum(mr, z, col[i]);
-          z *= wn;
+          for (int i = j; i < N; i += L) {
+            accum(s_mr[i], z, col[i]);
+            z *= wn;
+          }
+        } else {
+          double* w = s_w + grp * kTvlGaps;
+          for (int q = j; q < K; q += L) w[q] = exp(-(lam * s_gd[q]));
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 2
+          for (int i = j; i < N; i += L) {
+            const double2 mr = s_mr[i];
+            const double wn = w[s_gi[i]];
+            accum(mr, z, col[i]);
+            z *= wn;
+          }
         }
       } else {
 #pragma unroll 2
@@ -433,7 +452,7 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
         det = sgn * prod;
         // column qr of W (its upper triangle mirrored, as the replicated form uses it)
         double wc[M];
-        qd.mirror(x, wc);
+        qd.mirror<XDPP>(x, wc);
         double wq = 0.0;
 #pragma unroll
         for (int k = 0; k < M; ++k) wq = fma(wc[k], u[k], wq);
@@ -451,7 +470,7 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
 #pragma unroll
           for (int k = 0; k < M; ++k) pfc[k] = sigma2 * wc[k];
           quad_gather_rows<M>(pfc, Pf);
-          qd.propagate(bf, Pf, beta, Pc);
+          qd.propagate<XDPP>(bf, Pf, beta, Pc);
         }
       } else {
       double W[M][M];

@@ -94,6 +94,13 @@ __device__ __forceinline__ void dd_propagate(const double* par, const dd (&b)[M4
     }
 }
 
+// x of the lane at byte address `addr` (= lane · 4) of this wave (ds_bpermute: the LDS crossbar, no LDS memory)
+__device__ __forceinline__ double lane_read(int addr, double x) {
+  const int lo = __builtin_amdgcn_ds_bpermute(addr, __double2loint(x));
+  const int hi = __builtin_amdgcn_ds_bpermute(addr, __double2hiint(x));
+  return __hiloint2double(hi, lo);
+}
+
 // LDS writes of this wave visible to its own later reads (the quads of a filter are in one wave)
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -119,7 +126,9 @@ __device__ __forceinline__ void gather_sym(const dd (&col)[M4], dd (&X)[M4][M4])
 // the new P.  Every upper entry (i ≤ k) is formed by role k exactly as dd_propagate forms it, and the
 // entry below the diagonal is taken from the role that owns it as an upper entry, so P stays bitwise
 // symmetric and bitwise dd_propagate's.  X: the full symmetric matrix (every lane).
-// xch: this filter's 4×4 dd exchange block in LDS (the transpose of the new P's columns).
+// xch: this filter's 4×4 dd exchange block in LDS (the transpose of the new P's columns).  The transpose by quad DPP
+// exchanges instead (no wave barriers) measured slower even at L = 64, where the step is latency-bound (B = 1: 7.30 vs
+// 7.15 ms; profiles/r6/tvl_latency/run1): a dd lane-dependent select costs more than the barrier it removes.
 __device__ __forceinline__ void dd_propagate_q(const double* par, int qr, const dd (&b)[M4], const dd (&X)[M4][M4],
                                                bool scale, dd* xch, dd (&beta)[M4], dd (&Pc)[M4]) {
   const dd* Phi = reinterpret_cast<const dd*>(par + kDPhi);
@@ -513,6 +522,9 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
       if (K > 0) {
         dd* w = s_w + grp * kDdWStride;
         dd z;
+        // one jump equal to some lane's first maturity (uniform grids): the factor is that lane's start value,
+        // read across the group with ds_bpermute — no LDS block, no wave barrier on the step's serial path
+        const bool jump1 = pstep == 0.0 && K == 1 && s_gsrc[0] >= 0;  // block-uniform
         if (pstep > 0.0) {
           // power mode: one dd exp, b = e^{−λΔ}; the lane's start value and the group's jump factors are integer
           // powers of it (m_j/Δ and e_q are exact integers) — in place of one dd exp per maturity
@@ -523,14 +535,18 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
           z = (j < N) ? dd_exp(neg_rate(lam, s_m[j])) : dd_make(0.0);
           // a jump equal to some lane's first maturity (uniform grids: d = L·Δ = m_{L−1}) is that
           // lane's start value — the same dd_exp of the same argument — so only the others cost an exp
-          for (int q = 0; q < K; ++q)
-            if (s_gsrc[q] == j) w[q] = z;
-          for (int q = j; q < K; q += L)
-            if (s_gsrc[q] < 0) w[q] = dd_exp(neg_rate(lam, s_gd[q]));
+          if (!jump1) {
+            for (int q = 0; q < K; ++q)
+              if (s_gsrc[q] == j) w[q] = z;
+            for (int q = j; q < K; q += L)
+              if (s_gsrc[q] < 0) w[q] = dd_exp(neg_rate(lam, s_gd[q]));
+          }
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (!jump1) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
         // the LDS operands of maturity i + L are read while maturity i is accumulated (at one wave per SIMD a
         // read at the top of the iteration it feeds stalls the wave for the LDS latency); the last read is a
         // harmless repeat of maturity N − 1
@@ -540,7 +556,13 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
         dd rm_n = s_rm[i0];
         if (K == 1) {
           // one jump (uniform grids): the factor is loop-invariant
-          const dd wn = w[0];
+          dd wn;
+          if (jump1) {
+            const int src = ((tid & 63) - j + s_gsrc[0]) << 2;  // the source lane of this group (groups are wave-aligned)
+            wn = {lane_read(src, z.hi), lane_read(src, z.lo)};
+          } else {
+            wn = w[0];
+          }
           for (int i = j; i < N; i += L) {
             const double m = m_n, y = y_n;
             const dd rm = rm_n;
