@@ -90,6 +90,7 @@ __global__ __launch_bounds__(256) void tvl_init_kernel(const double* __restrict_
 struct TvlQuad {
   int qr;
   double phr[4], qc[4], dq;
+  double phi[4][4];  // Φ (every row: column qr of Φ Pf)
   double* xch;  // this group's 4×4 exchange block (LDS)
 
   // column qr of the symmetric matrix whose upper entries are `v[i]` for i ≤ qr (this role) and
@@ -111,9 +112,11 @@ struct TvlQuad {
     }
     wave_lds_sync();  // the block is rewritten by the next exchange
   }
-  // β ← δ + Φ bf;  P ← Φ Pf Φ' + Q  (propagate_state, filter.jl:162-176): Pf the full symmetric matrix
+  // β ← δ + Φ bf;  P ← Φ Pf Φ' + Q  (propagate_state, filter.jl:162-176), from pf = column qr of the symmetric Pf:
+  // role qr forms column qr of A = Φ Pf (the entry role i of the row form would form, in the same operation order),
+  // one gather hands every lane A, and role qr forms column qr of A Φ' + Q
   template <bool DPP>
-  __device__ __forceinline__ void propagate(const double (&bf)[4], const double (&Pf)[4][4], double (&beta)[4],
+  __device__ __forceinline__ void propagate(const double (&bf)[4], const double (&pf)[4], double (&beta)[4],
                                             double (&Pc)[4]) const {
     double bq = dq;
 #pragma unroll
@@ -122,21 +125,21 @@ struct TvlQuad {
     beta[1] = quad_bcast_f64<1>(bq);
     beta[2] = quad_bcast_f64<2>(bq);
     beta[3] = quad_bcast_f64<3>(bq);
-    double ar[4], A[4][4];
+    double ac[4], At[4][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int i = 0; i < 4; ++i) {
       double a = 0.0;
 #pragma unroll
-      for (int l = 0; l < 4; ++l) a = fma(phr[l], Pf[l][j], a);
-      ar[j] = a;
+      for (int l = 0; l < 4; ++l) a = fma(phi[i][l], pf[l], a);
+      ac[i] = a;
     }
-    quad_gather_rows<4>(ar, A);
+    quad_gather_rows<4>(ac, At);  // At[l][i] = A[i][l]
     double pc[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       double t = qc[i];
 #pragma unroll
-      for (int l = 0; l < 4; ++l) t = fma(A[i][l], phr[l], t);
+      for (int l = 0; l < 4; ++l) t = fma(At[l][i], phr[l], t);
       pc[i] = t;
     }
     mirror<DPP>(pc, Pc);
@@ -201,6 +204,8 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
     for (int i = 0; i < M; ++i) {
       beta[i] = r[kRecBeta + i];
       qd.phr[i] = r[kRecPhi + qd.qr * M + i];
+#pragma unroll
+      for (int k = 0; k < M; ++k) qd.phi[i][k] = r[kRecPhi + i * M + k];
       const int lo = i < qd.qr ? i : qd.qr, hi = i < qd.qr ? qd.qr : i;
       const int q = lo * M - lo * (lo - 1) / 2 + (hi - lo);  // upper-triangle record index
       qd.qc[i] = r[kRecQ + q];
@@ -268,19 +273,25 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
     load_chunk(1);
   }
 
+  // the staged column's NaN flag is read one step ahead: the branch at the top of a step would otherwise wait on
+  // an LDS read every step (at one wave per SIMD the latency is exposed)
+  double nan_next = nsteps > 0 ? s_nan[0] : 0.0;
   for (int t = 0; t < nsteps; ++t) {
     const int tt = t % TC;
     const bool act = t < my_steps;
     const bool acc = t >= 1;  // Julia t > 1 (filter.jl:194)
-    const bool nan_col = s_nan[tt] != 0.0 || t >= my_data;
+    const bool nan_col = nan_next != 0.0 || t >= my_data;
+    if (tt + 1 < TC) nan_next = s_nan[tt + 1];  // the next chunk's first flag is read after its store
     if (act && nan_col) {
       // filter.jl:13-29: prediction only; F, F⁻¹, v stale → the loglik re-adds the last term
       if constexpr (DIST) {
-        double bf[M], Pf[M][M];
+        double bf[M], pf[M];
 #pragma unroll
-        for (int i = 0; i < M; ++i) bf[i] = beta[i];
-        quad_gather_rows<M>(Pc, Pf);  // P symmetric: role S's column is row S
-        qd.propagate<XDPP>(bf, Pf, beta, Pc);
+        for (int i = 0; i < M; ++i) {
+          bf[i] = beta[i];
+          pf[i] = Pc[i];
+        }
+        qd.propagate<XDPP>(bf, pf, beta, Pc);
       } else {
         double bf[M], Pf[M][M];
 #pragma unroll
@@ -466,11 +477,10 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
         q = (vv - uk) * rsig2;
         upd = det != 0.0;  // inv(F) threw: return without updating (filter.jl:51-56)
         if (upd) {
-          double pfc[M], Pf[M][M];
+          double pfc[M];
 #pragma unroll
           for (int k = 0; k < M; ++k) pfc[k] = sigma2 * wc[k];
-          quad_gather_rows<M>(pfc, Pf);
-          qd.propagate<XDPP>(bf, Pf, beta, Pc);
+          qd.propagate<XDPP>(bf, pfc, beta, Pc);
         }
       } else {
       double W[M][M];
@@ -524,6 +534,7 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
       __syncthreads();
       store_chunk();
       __syncthreads();
+      nan_next = s_nan[0];
       load_chunk(t / TC + 2);
     }
   }

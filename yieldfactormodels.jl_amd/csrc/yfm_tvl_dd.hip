@@ -122,14 +122,15 @@ __device__ __forceinline__ void gather_sym(const dd (&col)[M4], dd (&X)[M4][M4])
 }
 
 // dd_propagate distributed over the quad (role qr = lane & 3; lanes of a group with the same role
-// compute the same values): β_qr then a broadcast; row qr of A = ΦX, broadcast; then column qr of
-// the new P.  Every upper entry (i ≤ k) is formed by role k exactly as dd_propagate forms it, and the
-// entry below the diagonal is taken from the role that owns it as an upper entry, so P stays bitwise
-// symmetric and bitwise dd_propagate's.  X: the full symmetric matrix (every lane).
+// compute the same values): β_qr then a broadcast; column qr of A = ΦX from column qr of X (the entry role i of the
+// row form would form, in the same operation order), one gather; then column qr of the new P.  Every upper entry
+// (i ≤ k) is formed by role k exactly as dd_propagate forms it, and the entry below the diagonal is taken from the
+// role that owns it as an upper entry, so P stays bitwise symmetric and bitwise dd_propagate's.  xc: column qr of
+// the symmetric X.
 // xch: this filter's 4×4 dd exchange block in LDS (the transpose of the new P's columns).  The transpose by quad DPP
 // exchanges instead (no wave barriers) measured slower even at L = 64, where the step is latency-bound (B = 1: 7.30 vs
 // 7.15 ms; profiles/r6/tvl_latency/run1): a dd lane-dependent select costs more than the barrier it removes.
-__device__ __forceinline__ void dd_propagate_q(const double* par, int qr, const dd (&b)[M4], const dd (&X)[M4][M4],
+__device__ __forceinline__ void dd_propagate_q(const double* par, int qr, const dd (&b)[M4], const dd (&xc)[M4],
                                                bool scale, dd* xch, dd (&beta)[M4], dd (&Pc)[M4]) {
   const dd* Phi = reinterpret_cast<const dd*>(par + kDPhi);
   const dd* Q = reinterpret_cast<const dd*>(par + kDQ);
@@ -143,24 +144,24 @@ __device__ __forceinline__ void dd_propagate_q(const double* par, int qr, const 
     beta[2] = quad_bcast<2>(s);
     beta[3] = quad_bcast<3>(s);
   }
-  dd A[M4][M4];
+  dd At[M4][M4];  // At[l][i] = A[i][l]
   {
-    dd Ar[M4];
+    dd Ac[M4];
 #pragma unroll
-    for (int j = 0; j < M4; ++j) {
+    for (int i = 0; i < M4; ++i) {
       dd_acc a;
 #pragma unroll
-      for (int l = 0; l < M4; ++l) a.add_prod(Phi[qr * M4 + l], X[l][j]);
-      Ar[j] = a.value();
+      for (int l = 0; l < M4; ++l) a.add_prod(Phi[i * M4 + l], xc[l]);
+      Ac[i] = a.value();
     }
-    gather_sym(Ar, A);  // row i of A from role i (not symmetric: bcast_row just moves rows)
+    gather_sym(Ac, At);  // role l's column l of A, in every lane
   }
   dd pc[M4];
 #pragma unroll
   for (int i = 0; i < M4; ++i) {
     dd_acc a;
 #pragma unroll
-    for (int l = 0; l < M4; ++l) a.add_prod(A[i][l], Phi[qr * M4 + l]);
+    for (int l = 0; l < M4; ++l) a.add_prod(At[l][i], Phi[qr * M4 + l]);
     dd s = a.value();
     if (scale) s = dd_mul(s, sig2);
     pc[i] = dd_add(s, Q[i <= qr ? utri(i, qr) : utri(qr, i)]);
@@ -429,18 +430,24 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
     load_chunk(1);
   }
 
+  // the staged column's NaN flag is read one step ahead: the branch at the top of a step would otherwise wait on
+  // an LDS read every step (at one wave per SIMD the latency is exposed)
+  double nan_next = nsteps > 0 ? s_nan[0] : 0.0;
   for (int t = 0; t < nsteps; ++t) {
     const int tt = t % TC;
     const bool act = live && t < my_steps;
     const bool acc = t >= 1;  // Julia t > 1 (filter.jl:194)
-    const bool nan_col = s_nan[tt] != 0.0 || t >= my_data;
+    const bool nan_col = nan_next != 0.0 || t >= my_data;
+    if (tt + 1 < TC) nan_next = s_nan[tt + 1];  // the next chunk's first flag is read after its store
     if (act && nan_col) {
       // filter.jl:13-29: prediction only; F, F⁻¹, v stale → the loglik re-adds the last term
-      dd bf[M4], X[M4][M4];
+      dd bf[M4], xc[M4];
 #pragma unroll
-      for (int i = 0; i < M4; ++i) bf[i] = beta[i];
-      gather_sym(Pc, X);
-      dd_propagate_q(par, qr, bf, X, false, xch, beta, Pc);
+      for (int i = 0; i < M4; ++i) {
+        bf[i] = beta[i];
+        xc[i] = Pc[i];
+      }
+      dd_propagate_q(par, qr, bf, xc, false, xch, beta, Pc);
       if (acc) {
         sum_ld.add(dd_make(last_ld));
         sum_q.add(dd_make(last_q));
@@ -685,9 +692,7 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
       const double dh = dd_to_double(det);
       const bool upd = dh != 0.0;  // inv(F) threw: return without updating (filter.jl:51-56)
       if (upd) {
-        dd Wf[M4][M4];
-        gather_sym(ws, Wf);
-        dd_propagate_q(par, qr, bf, Wf, true, xch, beta, Pc);
+        dd_propagate_q(par, qr, bf, ws, true, xch, beta, Pc);
       }
       last_ld = upd ? log(fabs(dh)) : -__builtin_inf();
       last_q = upd ? q : __builtin_nan("");
@@ -718,6 +723,7 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
       __syncthreads();
       store_chunk();
       __syncthreads();
+      nan_next = s_nan[0];
       load_chunk(t / TC + 2);
     }
   }
