@@ -759,8 +759,10 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(w, args.cpu_seconds, out_host)
+        ro1 = cpu["optimised"].get("evals_per_s_1_thread")
         cpu["gpu_over_cpu"] = {"dense_port": value / cpu["value"],
                                "optimised": value / cpu["optimised"]["evals_per_s"],
+                               "optimised_1_thread": value / ro1 if ro1 else None,
                                "optimised_extrapolated_all_physical_cores":
                                    (value / cpu["optimised"]["extrapolated_all_physical_cores"]
                                     if cpu["optimised"]["extrapolated_all_physical_cores"] else None)}
@@ -798,6 +800,11 @@ def main():
         if per_rank:
             line.update(per_rank)
         if fp64_mode:
+            if cpu and cpu["optimised"].get("evals_per_s_1_thread"):
+                # the FP64 mode against the optimised CPU filter, which computes in FP64 too
+                ro1 = cpu["optimised"]["evals_per_s_1_thread"]
+                fp64_mode["gpu_over_cpu"] = {"optimised": fp64_mode["evals_per_s"] / cpu["optimised"]["evals_per_s"],
+                                             "optimised_1_thread": fp64_mode["evals_per_s"] / ro1}
             line["fp64_mode"] = fp64_mode
         if steady:
             line["steady_state"] = steady

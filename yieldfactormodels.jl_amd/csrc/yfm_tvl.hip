@@ -278,7 +278,7 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
   double nan_next = nsteps > 0 ? s_nan[0] : 0.0;
   for (int t = 0; t < nsteps; ++t) {
     const int tt = t % TC;
-    const bool act = t < my_steps;
+    const bool act = live && t < my_steps;  // the tail block's padding groups skip the filter (B = 1: three of four waves)
     const bool acc = t >= 1;  // Julia t > 1 (filter.jl:194)
     const bool nan_col = nan_next != 0.0 || t >= my_data;
     if (tt + 1 < TC) nan_next = s_nan[tt + 1];  // the next chunk's first flag is read after its store
