@@ -91,6 +91,7 @@ struct yfm_ctx {
   // panel
   int N = 0, T = 0, np = 0, ldp = 0;
   DevBuf panel, mats, raw;
+  DevBuf colsum;  // the panel's dd column statistics (certified TVλ), made by yfm_set_panel
   // staging for host-pointer calls
   DevBuf theta, out, tuse, rec_beta, rec_P;
   DevBuf flags;  // 2 banks × kFlagsPerBank unsigned int: n_init_throw, n_neg_inf, deferral list length, n_deferred, steady wave-steps
@@ -350,11 +351,20 @@ int launch_impl(yfm_ctx* ctx, int kind, int space, const double* d_theta, int P,
     yfm::TvlGaps g;
     if (ctx->precision == YFM_PREC_CERTIFIED) {
       lanes = yfm::tvl_dd_lanes_for(B, ctx->N, std::getenv("YFM_TVL_LANES") ? lanes : 0, ctx->lane_share);
-      YFM_HIP_CHECK(w_scratch_dd.ensure(yfm::tvl_dd_scratch_bytes(B, a.T)));
+      // the context's panel has its column statistics already; a panel of the launch's own gets them here
+      const bool own_panel = pv && pv->raw != static_cast<const double*>(ctx->raw.p);
+      const size_t rec_bytes = yfm::tvl_dd_scratch_bytes(B);
+      YFM_HIP_CHECK(w_scratch_dd.ensure(rec_bytes + (own_panel ? yfm::tvl_dd_colsum_bytes(a.T) : 0)));
       double* rdd = static_cast<double*>(w_scratch_dd.p);
+      const double* colsum = static_cast<const double*>(ctx->colsum.p);
+      if (own_panel) {
+        double* cs = rdd + rec_bytes / sizeof(double);
+        YFM_HIP_CHECK(yfm::launch_tvl_dd_colsum(a.raw, a.N, a.T, cs, s));
+        colsum = cs;
+      }
       if (int r = tvl_gaps(ctx, lanes, g)) return r;
       e = yfm::launch_tvl_dd_init(a, rdd);
-      if (e == hipSuccess) e = yfm::launch_tvl_dd(a, rdd, g, lanes);
+      if (e == hipSuccess) e = yfm::launch_tvl_dd(a, rdd, colsum, g, lanes);
     } else {
       YFM_HIP_CHECK(w_scratch.ensure(yfm::tvl_scratch_bytes(B)));
       a.scratch = static_cast<double*>(w_scratch.p);
@@ -558,6 +568,9 @@ int yfm_set_panel(yfm_ctx* ctx, const double* Y, int N, int T, const double* mat
   YFM_HIP_CHECK(hipMemcpyAsync(ctx->mats.p, maturities, sizeof(double) * N, hipMemcpyHostToDevice, ctx->stream));
   YFM_HIP_CHECK(yfm::launch_prep_panel(static_cast<const double*>(ctx->raw.p), N, T, npad, ldp,
                                        static_cast<double*>(ctx->panel.p), ctx->stream));
+  YFM_HIP_CHECK(ctx->colsum.ensure(yfm::tvl_dd_colsum_bytes(T)));
+  YFM_HIP_CHECK(yfm::launch_tvl_dd_colsum(static_cast<const double*>(ctx->raw.p), N, T,
+                                          static_cast<double*>(ctx->colsum.p), ctx->stream));
   YFM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
   ctx->N = N;
   ctx->T = T;

@@ -72,13 +72,16 @@ hipError_t launch_tvl(const LaunchArgs& a, const TvlGaps& g, int lanes);
 constexpr int kRecSigma = 0, kRecDelta = 1, kRecPhi = 5, kRecQ = 21, kRecBeta = 31, kRecP = 35, kRecOk = 45;
 constexpr int kRecLen = 48;  // padded to 16-byte multiples
 // the same filter in double-double arithmetic (yfm_tvl_dd.hip), YFM_PREC_CERTIFIED: the init
-// kernel writes the per-candidate dd records and the panel's dd column sums into `rec_dd`
-// (tvl_dd_scratch_bytes(B, T));
+// kernel writes the per-candidate dd records into `rec_dd` (tvl_dd_scratch_bytes(B)); the panel's dd column
+// statistics (tvl_dd_colsum_bytes(T)) are made once per panel (yfm_set_panel) or, for a panel of its own
+// (get_loss_array's tiled one), by the launch into its scratch (colsum_out).
 // tvl_dd_lanes_for picks the lanes per filter (`want` > 0: a requested width, clamped; `share` as tvl_lanes_for)
-size_t tvl_dd_scratch_bytes(int B, int T);
+size_t tvl_dd_scratch_bytes(int B);
+size_t tvl_dd_colsum_bytes(int T);
 int tvl_dd_lanes_for(int B, int N, int want, int share = 1);
+hipError_t launch_tvl_dd_colsum(const double* Y, int N, int T, double* colsum, hipStream_t s);
 hipError_t launch_tvl_dd_init(const LaunchArgs& a, double* rec_dd);
-hipError_t launch_tvl_dd(const LaunchArgs& a, const double* rec_dd, const TvlGaps& g, int lanes);
+hipError_t launch_tvl_dd(const LaunchArgs& a, const double* rec_dd, const double* colsum, const TvlGaps& g, int lanes);
 // Trajectory outputs (yfm_predict.hip) from a recorded state trajectory.
 struct PredictArgs {
   int kind, M, L, N, P, B, T;

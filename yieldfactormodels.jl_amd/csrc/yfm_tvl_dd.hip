@@ -755,7 +755,7 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
 namespace {
 
 template <int L>
-hipError_t launch_tvl_dd_l(const LaunchArgs& a, const double* rec_dd, const TvlGaps& g, int TC) {
+hipError_t launch_tvl_dd_l(const LaunchArgs& a, const double* rec_dd, const double* colsum, const TvlGaps& g, int TC) {
   constexpr int GPB = kDdBlock / L;
   const int grid = (a.B + GPB - 1) / GPB;
   constexpr int kSumDd = 2;
@@ -771,7 +771,6 @@ hipError_t launch_tvl_dd_l(const LaunchArgs& a, const double* rec_dd, const TvlG
                                        (int)shmem);
     if (e != hipSuccess) return e;
   }
-  const double* colsum = rec_dd + (size_t)kDRecLen * (size_t)(a.B > 0 ? a.B : 1);
   // the exact jump table if there is one, else the power mode if the grid allows it, else one exp per maturity
   const bool pw = g.K == 0 && g.Kp > 0;
   hipLaunchKernelGGL(k, dim3(grid), dim3(kDdBlock), shmem, a.stream, rec_dd, a.B, a.raw, colsum, a.panel, a.ldp,
@@ -783,9 +782,14 @@ hipError_t launch_tvl_dd_l(const LaunchArgs& a, const double* rec_dd, const TvlG
 
 }  // namespace
 
-// per-candidate records, then the panel's column statistics (5 doubles per column: tvl_dd_colsum_kernel)
-size_t tvl_dd_scratch_bytes(int B, int T) {
-  return sizeof(double) * ((size_t)kDRecLen * (size_t)(B > 0 ? B : 1) + 5 * (size_t)(T > 0 ? T : 1));
+// per-candidate records
+size_t tvl_dd_scratch_bytes(int B) { return sizeof(double) * (size_t)kDRecLen * (size_t)(B > 0 ? B : 1); }
+// the panel's column statistics: 5 doubles per column (tvl_dd_colsum_kernel)
+size_t tvl_dd_colsum_bytes(int T) { return sizeof(double) * 5 * (size_t)(T > 0 ? T : 1); }
+
+hipError_t launch_tvl_dd_colsum(const double* Y, int N, int T, double* colsum, hipStream_t s) {
+  hipLaunchKernelGGL(tvl_dd_colsum_kernel, dim3((T + 63) / 64), dim3(64), 0, s, Y, N, T, colsum);
+  return hipGetLastError();
 }
 
 int tvl_dd_lanes_for(int B, int N, int want, int share) {
@@ -824,12 +828,11 @@ int tvl_dd_lanes_for(int B, int N, int want, int share) {
 hipError_t launch_tvl_dd_init(const LaunchArgs& a, double* rec_dd) {
   hipLaunchKernelGGL(tvl_dd_init_kernel, dim3((a.B + 63) / 64), dim3(64), 0, a.stream, a.theta, a.P, a.B, a.space,
                      rec_dd, a.flags_next);
-  hipLaunchKernelGGL(tvl_dd_colsum_kernel, dim3((a.T + 63) / 64), dim3(64), 0, a.stream, a.raw, a.N, a.T,
-                     rec_dd + (size_t)kDRecLen * (size_t)(a.B > 0 ? a.B : 1));
   return hipGetLastError();
 }
 
-hipError_t launch_tvl_dd(const LaunchArgs& a, const double* rec_dd, const TvlGaps& g_in, int lanes) {
+hipError_t launch_tvl_dd(const LaunchArgs& a, const double* rec_dd, const double* colsum, const TvlGaps& g_in,
+                         int lanes) {
   // the recurrence z_{i+L} = z_i·e^{−λ d} is only as exact as the jumps d: a rounded maturity
   // difference would put an FP64-sized error into every loading, so such grids take one dd exp
   // per maturity
@@ -839,11 +842,11 @@ hipError_t launch_tvl_dd(const LaunchArgs& a, const double* rec_dd, const TvlGap
   if (TC > 32) TC = 32;
   if (TC < 1) return hipErrorInvalidValue;
   switch (lanes) {
-    case 4: return launch_tvl_dd_l<4>(a, rec_dd, g, TC);
-    case 8: return launch_tvl_dd_l<8>(a, rec_dd, g, TC);
-    case 16: return launch_tvl_dd_l<16>(a, rec_dd, g, TC);
-    case 32: return launch_tvl_dd_l<32>(a, rec_dd, g, TC);
-    case 64: return launch_tvl_dd_l<64>(a, rec_dd, g, TC);
+    case 4: return launch_tvl_dd_l<4>(a, rec_dd, colsum, g, TC);
+    case 8: return launch_tvl_dd_l<8>(a, rec_dd, colsum, g, TC);
+    case 16: return launch_tvl_dd_l<16>(a, rec_dd, colsum, g, TC);
+    case 32: return launch_tvl_dd_l<32>(a, rec_dd, colsum, g, TC);
+    case 64: return launch_tvl_dd_l<64>(a, rec_dd, colsum, g, TC);
   }
   return hipErrorInvalidValue;
 }
