@@ -304,7 +304,7 @@ __global__ __launch_bounds__(64) void tvl_dd_colsum_kernel(const double* __restr
   colsum[4 * (size_t)t + 3] = b.lo;
 }
 
-template <int L, bool RECORD>
+template <int L, bool RECORD, bool LONG = false>
 __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
     const double* __restrict__ rec, int B, const double* __restrict__ Y, const double* __restrict__ colsum,
     const double* __restrict__ prep, int ldp,
@@ -371,6 +371,7 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
 
   // the 4×4 update is distributed over the lanes of each quad: role qr holds column qr of P
   const int qr = tid & 3;
+  constexpr int kUnrollK1 = LONG ? 2 : 1;  // the one-jump maturity loop (below)
   dd* xch = s_xch + grp * kXchStride;
   dd beta[M4], Pc[M4];
 #pragma unroll
@@ -556,7 +557,10 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
         }
         // the LDS operands of maturity i + L are read while maturity i is accumulated (at one wave per SIMD a
         // read at the top of the iteration it feeds stalls the wave for the LDS latency); the last read is a
-        // harmless repeat of maturity N − 1
+        // harmless repeat of maturity N − 1.  LONG (≥ 32 maturities per lane: config 3's 90 at L = 4): the one-jump
+        // loop unrolled by two, the register sets alternating instead of being moved (136 → 126.5 instructions per
+        // maturity, 19.3 → 19.0 ms); short loops (L = 64 at N = 360, the estimator's N = 30 rounds) keep the plain
+        // instantiation — the unrolled one measured 2–4% slower there (profiles/r6/tvl_latency/c20/, c20b/)
         const int last = N - 1;
         const int i0 = min(j, last);
         double m_n = s_m[i0], y_n = col[i0];
@@ -570,6 +574,7 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
           } else {
             wn = w[0];
           }
+#pragma unroll kUnrollK1
           for (int i = j; i < N; i += L) {
             const double m = m_n, y = y_n;
             const dd rm = rm_n;
@@ -766,6 +771,9 @@ hipError_t launch_tvl_dd_l(const LaunchArgs& a, const double* rec_dd, const doub
                        sizeof(int) * a.N;
   if (shmem > 160 * 1024) return hipErrorInvalidValue;  // gfx950: 160 KiB of LDS per workgroup
   auto* k = a.rec_beta ? &tvl_dd_loglik_kernel<L, true> : &tvl_dd_loglik_kernel<L, false>;
+  if constexpr (L <= 8) {
+    if (!a.rec_beta && a.N >= 32 * L) k = &tvl_dd_loglik_kernel<L, false, true>;  // long maturity loops
+  }
   if (shmem > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)shmem);
