@@ -372,6 +372,7 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
   // the 4×4 update is distributed over the lanes of each quad: role qr holds column qr of P
   const int qr = tid & 3;
   constexpr int kUnrollK1 = LONG ? 2 : 1;  // the one-jump maturity loop (below)
+  constexpr bool FACT = L <= 8;              // 1/λ factored out of the z2 sums (below)
   dd* xch = s_xch + grp * kXchStride;
   dd beta[M4], Pc[M4];
 #pragma unroll
@@ -473,14 +474,18 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
       // basis (z2, z, z4) — z3 = z2 − z is recovered per step below.  The innovation sums are
       // recovered per step too: u = Z'y − Z'Z[:,1:3]β[1:3] and v'v = y'y − y'ŷ − ŷ'v, which in
       // dd keeps ≥ 80 of 106 bits where the FP64 kernel (yfm_tvl.hip) forms v per maturity.
-      // The sums of z, z2 and their products with each other and with y are σ-split accumulations
+      // FACT (L ≤ 8): z2 = (1 − z)/(λm) = w2/λ with w2 = (1 − z)/m — the lanes accumulate w2 and its products and
+      // the group sums are scaled by 1/λ (1/λ² for Σ w2²) once per step, one dd product per maturity fewer (config 3
+      // 19.06 → 17.76 ms); at L = 64 (six maturities per lane, the step latency-bound) it measured 5% slower
+      // (profiles/r6/tvl_latency/c24/), so the wide groups keep z2 per maturity.
+      // The sums of z, z2 (w2) and their products with each other and with y are σ-split accumulations
       // (yfm_dd.hpp: dd_acc::add_sx): per step and lane, a tight bound on the terms over this lane's
-      // maturities (z = e^{−λm} ≤ e^{−λ m_min}, z2 = (1 − z)/(λm) ≤ min(1, 1/(λ m_min)), |y| ≤ the
-      // column's max) fixes the split constant.
+      // maturities (z = e^{−λm} ≤ e^{−λ m_min}, z2 = (1 − z)/(λm) ≤ min(1, 1/(λ m_min)), w2 ≤ min(1/m_min, λ),
+      // |y| ≤ the column's max) fixes the split constant.
       const double lamh = lam.hi, rlh = rl.hi;
       constexpr double kSlack = 1.0 + 0x1p-30;
       const double Be = exp(-(lamh * l_minm)) * kSlack;
-      const double Bz2 = fmin(1.0, rlh * l_rminm) * kSlack;
+      const double Bz2 = (FACT ? fmin(l_rminm, lamh) : fmin(1.0, rlh * l_rminm)) * kSlack;
       const double By = s_ymax[tt] * l_n;
       // t = k1 − kr/m + c2·m per maturity, σ-split with the bound of its three terms (k1's split once per step)
       const double sgt = split_const((fabs(k1.hi) + fabs(kr.hi) * l_rminm + fabs(c2.hi) * l_maxm) * kSlack);
@@ -497,11 +502,10 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
       const double sy2 = split_const(By * Bz2), syz = split_const(By * Be);
       dd_acc S2, Sz, S4, G22, G2z, G24, Gzz, Gz4, G44, Y2, Yz, Y4;
       auto accum = [&](double m, double y, dd rm, dd z) {
-        const dd it = dd_mul_nn(rl, rm);  // 1/τ
-        // 1 − z exactly (Fast2Sum: 1 ≥ z.hi), then (1 − z)/τ
+        // 1 − z exactly (Fast2Sum: 1 ≥ z.hi), then z2 = (1 − z)/τ (FACT: w2 = (1 − z)/m = λ·z2)
         const double o1 = 1.0 - z.hi;
         const dd ome = {o1, ((1.0 - o1) - z.hi) - z.lo};
-        const dd z2 = dd_mul_nn(ome, it);
+        const dd z2 = FACT ? dd_mul_nn(ome, rm) : dd_mul_nn(ome, dd_mul_nn(rl, rm));
         // ((β2+β3)(z/λ − z/(λ²m)) + β3·m·z)·(λ − 0.01) = z·t,  t = k1(1 − 1/τ) + c2·m
         // (t left unnormalised: its products are formed to an absolute error of ~2^-104·|terms|)
         dd ta;
@@ -583,7 +587,7 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
             y_n = col[in];
             rm_n = s_rm[in];
             accum(m, y, rm, z);
-            z = dd_mul(z, wn);
+            z = FACT ? dd_mul_nn(z, wn) : dd_mul(z, wn);  // FACT: left unnormalised (z only feeds products, σ-split sums and 1 − z)
           }
         } else {
           dd wn_n = w[s_gi[i0]];
@@ -596,16 +600,25 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
             rm_n = s_rm[in];
             wn_n = w[s_gi[in]];
             accum(m, y, rm, z);
-            z = dd_mul(z, wn);
+            z = FACT ? dd_mul_nn(z, wn) : dd_mul(z, wn);  // FACT: left unnormalised (z only feeds products, σ-split sums and 1 − z)
           }
         }
       } else {
         for (int i = j; i < N; i += L) accum(s_m[i], col[i], s_rm[i], dd_exp(neg_rate(lam, s_m[i])));
       }
-      const dd s2 = group_sum_acc<L>(S2), sz = group_sum_acc<L>(Sz), s4 = group_sum_acc<L>(S4);
-      const dd g22 = group_sum_acc<L>(G22), g2z = group_sum_acc<L>(G2z), g24 = group_sum_acc<L>(G24);
+      dd s2 = group_sum_acc<L>(S2), g22 = group_sum_acc<L>(G22), g2z = group_sum_acc<L>(G2z);
+      dd g24 = group_sum_acc<L>(G24), y2 = group_sum_acc<L>(Y2);
+      if constexpr (FACT) {
+        const dd rl2 = dd_mul(rl, rl);
+        s2 = dd_mul(s2, rl);
+        g22 = dd_mul(g22, rl2);
+        g2z = dd_mul(g2z, rl);
+        g24 = dd_mul(g24, rl);
+        y2 = dd_mul(y2, rl);
+      }
+      const dd sz = group_sum_acc<L>(Sz), s4 = group_sum_acc<L>(S4);
       const dd gzz = group_sum_acc<L>(Gzz), gz4 = group_sum_acc<L>(Gz4), g44 = group_sum_acc<L>(G44);
-      const dd y2 = group_sum_acc<L>(Y2), yz = group_sum_acc<L>(Yz), y4 = group_sum_acc<L>(Y4);
+      const dd yz = group_sum_acc<L>(Yz), y4 = group_sum_acc<L>(Y4);
       // back to the loading basis (1, z2, z3 = z2 − z, z4)
       const dd g23 = dd_sub(g22, g2z);
       dd G[M4][M4];
