@@ -261,12 +261,16 @@ def test_tvl_power_mode_wu30_t600(engine, L):
     assert int((e_pw > EXACT).sum()) <= int((e_ex > EXACT).sum()) + 1
 
 
-@pytest.mark.parametrize("grid", ["wu30", "irregular"])
+@pytest.mark.parametrize("grid", ["wu30", "irregular", "quarters"])
 def test_tvl_maturity_grids_and_exp_paths(engine, grid):
     """The exp recurrence over maturity jumps (≤ 8 distinct m_{i+L} − m_i) vs one exp per maturity
-    (YFM_TVL_EXP=1, also the automatic fallback for irregular grids), both precisions."""
+    (YFM_TVL_EXP=1, also the automatic fallback for irregular grids), both precisions; "quarters" (maturities k/4
+    years: exact differences, not integers, one jump) takes the certified kernel's exact table with the jump factor
+    read across the group by ds_bpermute."""
     if grid == "wu30":
         mats = S.maturities_30()
+    elif grid == "quarters":
+        mats = 0.25 * np.arange(1, 121, dtype=np.float64)
     else:
         mats = np.sort(np.random.default_rng(3).uniform(1.0, 360.0, 24)).round(3)
     Y = S.simulate_panel(KIND_TVL, 80, maturities=mats)
