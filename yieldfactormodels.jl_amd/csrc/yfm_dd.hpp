@@ -28,108 +28,108 @@ struct dd {
   double hi, lo;
 };
 
-__device__ __forceinline__ dd dd_make(double x) { return {x, 0.0}; }
+__host__ __device__ __forceinline__ dd dd_make(double x) { return {x, 0.0}; }
 
 // s + e = a + b exactly (any magnitudes)
-__device__ __forceinline__ dd two_sum(double a, double b) {
+__host__ __device__ __forceinline__ dd two_sum(double a, double b) {
   const double s = a + b;
   const double bb = s - a;
   const double e = (a - (s - bb)) + (b - bb);
   return {s, e};
 }
 // s + e = a + b exactly, requires |a| ≥ |b| (or a = 0)
-__device__ __forceinline__ dd fast_two_sum(double a, double b) {
+__host__ __device__ __forceinline__ dd fast_two_sum(double a, double b) {
   const double s = a + b;
   return {s, b - (s - a)};
 }
 // p + e = a·b exactly
-__device__ __forceinline__ dd two_prod(double a, double b) {
+__host__ __device__ __forceinline__ dd two_prod(double a, double b) {
   const double p = a * b;
   return {p, __builtin_fma(a, b, -p)};
 }
 
-__device__ __forceinline__ dd dd_neg(dd x) { return {-x.hi, -x.lo}; }
+__host__ __device__ __forceinline__ dd dd_neg(dd x) { return {-x.hi, -x.lo}; }
 
 // x + y, absolute error ≤ ~3u²(|x| + |y|)
-__device__ __forceinline__ dd dd_add(dd x, dd y) {
+__host__ __device__ __forceinline__ dd dd_add(dd x, dd y) {
   dd s = two_sum(x.hi, y.hi);
   s.lo += x.lo + y.lo;
   return fast_two_sum(s.hi, s.lo);
 }
-__device__ __forceinline__ dd dd_sub(dd x, dd y) { return dd_add(x, dd_neg(y)); }
+__host__ __device__ __forceinline__ dd dd_sub(dd x, dd y) { return dd_add(x, dd_neg(y)); }
 // x + d (d a double)
-__device__ __forceinline__ dd dd_add_d(dd x, double d) {
+__host__ __device__ __forceinline__ dd dd_add_d(dd x, double d) {
   dd s = two_sum(x.hi, d);
   s.lo += x.lo;
   return fast_two_sum(s.hi, s.lo);
 }
 // x·y, relative error ≤ 5u²
-__device__ __forceinline__ dd dd_mul(dd x, dd y) {
+__host__ __device__ __forceinline__ dd dd_mul(dd x, dd y) {
   dd p = two_prod(x.hi, y.hi);
   p.lo = __builtin_fma(x.hi, y.lo, __builtin_fma(x.lo, y.hi, p.lo));
   return fast_two_sum(p.hi, p.lo);
 }
 // x·y left unnormalised (|lo| ≤ ~3u|hi|): for products that only feed sums and products,
 // whose error-free steps do not need a normalised operand
-__device__ __forceinline__ dd dd_mul_nn(dd x, dd y) {
+__host__ __device__ __forceinline__ dd dd_mul_nn(dd x, dd y) {
   dd p = two_prod(x.hi, y.hi);
   p.lo = __builtin_fma(x.hi, y.lo, __builtin_fma(x.lo, y.hi, p.lo));
   return p;
 }
 // x·d
-__device__ __forceinline__ dd dd_mul_d(dd x, double d) {
+__host__ __device__ __forceinline__ dd dd_mul_d(dd x, double d) {
   dd p = two_prod(x.hi, d);
   p.lo = __builtin_fma(x.lo, d, p.lo);
   return fast_two_sum(p.hi, p.lo);
 }
 // exact scaling by a power of two
-__device__ __forceinline__ dd dd_ldexp(dd x, int k) { return {__builtin_ldexp(x.hi, k), __builtin_ldexp(x.lo, k)}; }
+__host__ __device__ __forceinline__ dd dd_ldexp(dd x, int k) { return {__builtin_ldexp(x.hi, k), __builtin_ldexp(x.lo, k)}; }
 // 1 / y: FP64 seed + one Newton step in dd (relative error ~ u²)
-__device__ __forceinline__ dd dd_rcp(dd y) {
+__host__ __device__ __forceinline__ dd dd_rcp(dd y) {
   const double r0 = 1.0 / y.hi;
   const dd e = dd_add_d(dd_neg(dd_mul_d(y, r0)), 1.0);  // 1 − y·r0
   return dd_add_d(dd_mul_d(e, r0), r0);                  // r0 + r0·e
 }
-__device__ __forceinline__ dd dd_div(dd x, dd y) { return dd_mul(x, dd_rcp(y)); }
-__device__ __forceinline__ double dd_to_double(dd x) { return x.hi + x.lo; }
+__host__ __device__ __forceinline__ dd dd_div(dd x, dd y) { return dd_mul(x, dd_rcp(y)); }
+__host__ __device__ __forceinline__ double dd_to_double(dd x) { return x.hi + x.lo; }
 
 // Accumulator with deferred normalisation: Σ terms kept as an exact leading sum (TwoSum) and
 // a plain FP64 sum of all trailing parts.  Same accuracy class as repeated dd_add for the
 // sums here (≤ a few hundred terms), at 8 ops per dd term instead of 11.
 struct dd_acc {
   double hi = 0.0, lo = 0.0;
-  __device__ __forceinline__ void add(dd x) {
+  __host__ __device__ __forceinline__ void add(dd x) {
     const dd s = two_sum(hi, x.hi);
     hi = s.hi;
     lo += s.lo + x.lo;
   }
   // += a·b without normalising the product
-  __device__ __forceinline__ void add_prod(dd a, dd b) {
+  __host__ __device__ __forceinline__ void add_prod(dd a, dd b) {
     dd p = two_prod(a.hi, b.hi);
     p.lo = __builtin_fma(a.hi, b.lo, __builtin_fma(a.lo, b.hi, p.lo));
     add(p);
   }
   // += a·d (d a double)
-  __device__ __forceinline__ void add_prod_d(dd a, double d) {
+  __host__ __device__ __forceinline__ void add_prod_d(dd a, double d) {
     dd p = two_prod(a.hi, d);
     p.lo = __builtin_fma(a.lo, d, p.lo);
     add(p);
   }
-  __device__ __forceinline__ dd value() const { return two_sum(hi, lo); }  // |lo| may exceed |hi| after cancellation
+  __host__ __device__ __forceinline__ dd value() const { return two_sum(hi, lo); }  // |lo| may exceed |hi| after cancellation
 
   // σ-split accumulation (Rump, Ogita & Oishi's ExtractScalar): with σ a power of two ≥ n·max|x.hi|
   // over the n terms this accumulator will receive, q = (σ + x.hi) − σ is x.hi rounded to a multiple
   // of ulp(σ) and x.hi − q is exact; every partial sum of the q's is a multiple of ulp(σ) below 2σ, so
   // `hi` stays exact with one plain addition instead of a TwoSum.  The absolute error, ≈ n²·ulp(σ)·u,
   // is in the same class as add()'s (the sums here have ≤ a few hundred terms).
-  __device__ __forceinline__ void add_sx(dd x, double sg) {
+  __host__ __device__ __forceinline__ void add_sx(dd x, double sg) {
     const double q = (sg + x.hi) - sg;
     hi += q;
     lo += (x.hi - q) + x.lo;
   }
   // += a·b: q = fl(σ + a.hi·b.hi) − σ (one FMA: the exact product rounded to a multiple of ulp(σ)),
   // a.hi·b.hi − q to one rounding (|·| ≤ ulp(σ)), plus the cross terms
-  __device__ __forceinline__ void add_prod_sx(dd a, dd b, double sg) {
+  __host__ __device__ __forceinline__ void add_prod_sx(dd a, dd b, double sg) {
     const double q = __builtin_fma(a.hi, b.hi, sg) - sg;
     hi += q;
     lo += __builtin_fma(a.hi, b.hi, -q);
@@ -137,7 +137,7 @@ struct dd_acc {
     lo = __builtin_fma(a.lo, b.hi, lo);
   }
   // += a·d (d a double)
-  __device__ __forceinline__ void add_prod_d_sx(dd a, double d, double sg) {
+  __host__ __device__ __forceinline__ void add_prod_d_sx(dd a, double d, double sg) {
     const double q = __builtin_fma(a.hi, d, sg) - sg;
     hi += q;
     lo += __builtin_fma(a.hi, d, -q);
@@ -147,59 +147,49 @@ struct dd_acc {
 
 // the split constant for add_sx & co.: a power of two ≥ x (x = terms × bound on |term|); 1 for
 // x = 0 and 2^1000 for a non-finite bound (the split then degrades to FP64 accumulation into lo)
-__device__ __forceinline__ double split_const(double x) {
+__host__ __device__ __forceinline__ double split_const(double x) {
   if (!(x <= 0x1p1000)) return 0x1p1000;
   return __builtin_ldexp(1.0, __builtin_amdgcn_frexp_exp(x));
 }
 
-// exp of a dd argument to ~2u² relative: x = k·ln2 + r, |r| ≤ ln2/2, e^r from a degree-9
-// Taylor polynomial of r/2^9 followed by 9 squarings of (1 + s) carried as s ← s(2 + s).
+// exp of a dd argument: x = (4096·m + 64·j1 + j2)·ln2/4096 + r, |r| ≤ ln2/8192, e^x = 2^m · 2^(j1/64) · 2^(j2/4096)
+// · e^r with both powers of two from a 128-entry dd table (yfm_exp_table.inc, correctly rounded) and e^r − 1 from a
+// degree-7 Taylor polynomial (its degree-4..7 tail in FP64: those terms are below 2^-54 of the result) — ≈ 125
+// operations instead of the ≈ 320 of the reduction to |r| ≤ ln2/1024 followed by nine squarings it replaced (round 6;
+// `tools/dd_exp_check.cpp` measures both against binary128 on 10⁶ arguments).  Relative error ≲ 4u² for |x| ≲ 40, and
+// the reduction's k·(ln2/4096)_lo rounding (absolute in r) up to ≈ 2⁻⁹⁸ at |x| ≈ 700 — the class of the old one.
 // Arguments beyond the FP64 range give 0 / Inf like exp(); NaN propagates.
-__device__ __forceinline__ dd dd_exp(dd x) {
-  constexpr double kLn2Hi = 0.6931471805599453094172321214581766;  // nearest double to ln 2
-  constexpr double kLn2Lo = 2.3190468138462996154e-17;             // ln 2 − kLn2Hi
+static __constant__ double kDdExpTab[128][2] = {
+#include "yfm_exp_table.inc"
+};
+__host__ __device__ __forceinline__ dd dd_exp_core(dd x, const double (*tab)[2]) {
+  constexpr double kInvC = 5909.2788874811944;          // 4096/ln 2
+  constexpr double kCHi = 0.0001692253858788929;        // nearest double to ln2/4096
+  constexpr double kCLo = 5.661735385366942e-21;        // ln2/4096 − kCHi
   if (!(x.hi > -745.2)) return {x.hi != x.hi ? x.hi : 0.0, 0.0};
   if (x.hi > 709.8) return {__builtin_inf(), 0.0};
-  const double k = __builtin_rint(x.hi * 1.4426950408889634073599);
-  // r = x − k·ln2 with k·ln2_hi exact (TwoProd)
-  const dd kh = two_prod(k, kLn2Hi);
-  dd r = dd_sub(x, kh);
-  r = dd_add_d(r, -k * kLn2Lo);
-  r = dd_ldexp(r, -9);
-  // s = e^r − 1 = r + r²/2! + … + r⁹/9!  (Horner on 1/n!)
-  constexpr double inv_fact[10] = {1.0,
-                                   1.0,
-                                   0.5,
-                                   1.6666666666666666574e-01,
-                                   4.1666666666666664354e-02,
-                                   8.3333333333333332177e-03,
-                                   1.3888888888888889419e-03,
-                                   1.9841269841269841253e-04,
-                                   2.4801587301587301566e-05,
-                                   2.7557319223985892511e-06};
-  constexpr double inv_fact_lo[10] = {0.0,
-                                      0.0,
-                                      0.0,
-                                      9.2518585385429706566e-18,
-                                      2.3129646346357426641e-18,
-                                      1.1564823173178713802e-19,
-                                      -5.3005439543735770590e-20,
-                                      1.7209558293420705286e-22,
-                                      2.1511947866775881608e-23,
-                                      -1.8583932740464720810e-22};
-  dd p = {inv_fact[9], inv_fact_lo[9]};
-#pragma unroll
-  for (int n = 8; n >= 1; --n) p = dd_add(dd_mul(p, r), dd{inv_fact[n], inv_fact_lo[n]});
-  dd s = dd_mul(p, r);
-#pragma unroll
-  for (int i = 0; i < 9; ++i) s = dd_mul(s, dd_add_d(s, 2.0));
-  const dd e = dd_add_d(s, 1.0);
-  return dd_ldexp(e, (int)k);
+  const double k = __builtin_rint(x.hi * kInvC);
+  const int ki = (int)k;
+  const int m = ki >> 12;                    // floor(k / 4096)
+  const int j1 = (ki >> 6) & 63, j2 = ki & 63;
+  dd r = dd_sub(x, two_prod(k, kCHi));       // k·C_hi exactly
+  r = dd_add_d(r, -k * kCLo);
+  // e^r − 1 = r·q1, q1 = 1 + r/2 + r²/6 + r³·(1/24 + r/120 + r²/720 + r³/5040)
+  const double q4 = __builtin_fma(r.hi, __builtin_fma(r.hi, __builtin_fma(r.hi, 1.9841269841269841e-4, 1.3888888888888889e-3),
+                                                      8.3333333333333332e-3), 4.1666666666666664e-2);
+  const dd q3 = dd_add(dd{0.16666666666666666, 9.25185853854297e-18}, dd_mul_d(r, q4));
+  const dd q2 = dd_add_d(dd_mul(r, q3), 0.5);
+  const dd q1 = dd_add_d(dd_mul(r, q2), 1.0);
+  const dd s = dd_mul(r, q1);
+  const dd t = dd_mul(dd{tab[j1][0], tab[j1][1]}, dd{tab[64 + j2][0], tab[64 + j2][1]});
+  const dd e = dd_add(t, dd_mul(t, s));
+  return dd_ldexp(e, m);
 }
+__device__ __forceinline__ dd dd_exp(dd x) { return dd_exp_core(x, kDdExpTab); }
 
 // x^n, n ≥ 0, by binary powering: ⌈log2 n⌉ squarings and popcount(n) products, relative error ≲ (2 log2 n + 2)·4u²
 // on top of n times x's own (the TVλ dd filter's e^{−λkΔ} = (e^{−λΔ})^k on integer maturity grids)
-__device__ __forceinline__ dd dd_powi(dd x, int n) {
+__host__ __device__ __forceinline__ dd dd_powi(dd x, int n) {
   dd r = dd_make(1.0);
   while (n > 0) {  // data-dependent trip count (≤ 9 for n < 512)
     if (n & 1) r = dd_mul(r, x);
@@ -213,7 +203,7 @@ __device__ __forceinline__ dd dd_powi(dd x, int n) {
 
 // −λ·m in dd for exp(−λm); a product that overflows (λ near the FP64 range) is −Inf, whose exp is
 // 0 as in the reference — TwoProd's error term would be Inf − Inf = NaN there
-__device__ __forceinline__ dd neg_rate(dd lam, double m) {
+__host__ __device__ __forceinline__ dd neg_rate(dd lam, double m) {
   const dd p = dd_mul_d(lam, m);
   return __builtin_isfinite(p.hi) ? dd_neg(p) : dd{-(lam.hi * m), 0.0};
 }
@@ -221,7 +211,7 @@ __device__ __forceinline__ dd neg_rate(dd lam, double m) {
 // Gaussian elimination with partial pivoting (first max |hi|, the getf2 rule) on an n×n dd
 // system with R right-hand sides; false on an exact zero pivot (where getrf reports info > 0).
 template <int n, int R>
-__device__ __forceinline__ bool dd_gauss(dd (&A)[n][n], dd (&X)[n][R], dd* det_out = nullptr) {
+__host__ __device__ __forceinline__ bool dd_gauss(dd (&A)[n][n], dd (&X)[n][R], dd* det_out = nullptr) {
   bool ok = true;
   double sgn = 1.0;
   dd det = dd_make(1.0);
@@ -282,7 +272,7 @@ __device__ __forceinline__ bool dd_gauss(dd (&A)[n][n], dd (&X)[n][R], dd* det_o
 }
 
 // log of a positive dd to ~u² absolute: FP64 seed + one Newton step on e^y = x
-__device__ __forceinline__ dd dd_log(dd x) {
+__host__ __device__ __forceinline__ dd dd_log(dd x) {
   const double y0 = log(x.hi);
   const dd e = dd_exp(dd_make(-y0));
   const dd t = dd_add_d(dd_mul(x, e), -1.0);  // x·e^{−y0} − 1
@@ -290,7 +280,7 @@ __device__ __forceinline__ dd dd_log(dd x) {
 }
 
 // transformations.jl:21-26 as written (2y/(1+y) − 1), in dd
-__device__ __forceinline__ dd dd_from_R_to_11(double x) {
+__host__ __device__ __forceinline__ dd dd_from_R_to_11(double x) {
   const dd y = dd_exp(dd_make(x));
   if (!(y.hi < __builtin_inf())) return {__builtin_nan(""), 0.0};  // Inf/Inf
   return dd_add_d(dd_div(dd_mul_d(y, 2.0), dd_add_d(y, 1.0)), -1.0);
@@ -303,7 +293,7 @@ __device__ __forceinline__ dd dd_from_R_to_11(double x) {
 // first, so (own, partner) and (partner, own) give the same bits (round 6: the lane-order selects,
 // 8 v_cndmask per value and level, are gone; logliks bitwise unchanged).
 template <int LVL>
-__device__ __forceinline__ void pair_exchange(double x, double& a, double& b) {
+__host__ __device__ __forceinline__ void pair_exchange(double x, double& a, double& b) {
   const int lo = __double2loint(x), hi = __double2hiint(x);
   if constexpr (LVL <= 3) {
     constexpr int ctrl = LVL == 0 ? 0xB1 : LVL == 1 ? 0x4E : LVL == 2 ? 0x141 : 0x140;
@@ -326,26 +316,26 @@ __device__ __forceinline__ void pair_exchange(double x, double& a, double& b) {
 
 // ---- quad exchanges for the lane-distributed 4×4 update (role c = lane & 3 inside each quad) ----
 template <int CTRL>
-__device__ __forceinline__ double quad_dpp(double x) {
+__host__ __device__ __forceinline__ double quad_dpp(double x) {
   const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), CTRL, 0xf, 0xf, true);
   const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), CTRL, 0xf, 0xf, true);
   return __hiloint2double(hi, lo);
 }
 // the value held by role S of this lane's quad
 template <int S>
-__device__ __forceinline__ dd quad_bcast(dd x) {
+__host__ __device__ __forceinline__ dd quad_bcast(dd x) {
   constexpr int ctrl = S | (S << 2) | (S << 4) | (S << 6);
   return {quad_dpp<ctrl>(x.hi), quad_dpp<ctrl>(x.lo)};
 }
 // the value held by role c ^ R (R = 1, 2, 3)
 template <int R>
-__device__ __forceinline__ dd quad_xor(dd x) {
+__host__ __device__ __forceinline__ dd quad_xor(dd x) {
   constexpr int ctrl = (0 ^ R) | ((1 ^ R) << 2) | ((2 ^ R) << 4) | ((3 ^ R) << 6);
   return {quad_dpp<ctrl>(x.hi), quad_dpp<ctrl>(x.lo)};
 }
 // v[i] for a lane-dependent i in [0, 4): a two-level mux on the bits of i (a chain of i == k selects is turned
 // into a scratch-indexed load by the compiler)
-__device__ __forceinline__ dd sel4(const dd (&v)[4], int i) {
+__host__ __device__ __forceinline__ dd sel4(const dd (&v)[4], int i) {
   const bool b0 = (i & 1) != 0, b1 = (i & 2) != 0;
   const dd lo = b0 ? v[1] : v[0];
   const dd hi = b0 ? v[3] : v[2];
@@ -353,7 +343,7 @@ __device__ __forceinline__ dd sel4(const dd (&v)[4], int i) {
 }
 
 template <int LVL>
-__device__ __forceinline__ void acc_level(double& hi, double& lo) {
+__host__ __device__ __forceinline__ void acc_level(double& hi, double& lo) {
   double h0, h1, l0, l1;
   pair_exchange<LVL>(hi, h0, h1);
   pair_exchange<LVL>(lo, l0, l1);
@@ -363,7 +353,7 @@ __device__ __forceinline__ void acc_level(double& hi, double& lo) {
 }
 
 template <int L>
-__device__ __forceinline__ dd group_sum_acc(dd_acc a) {
+__host__ __device__ __forceinline__ dd group_sum_acc(dd_acc a) {
   double hi = a.hi, lo = a.lo;
   if constexpr (L >= 2) acc_level<0>(hi, lo);
   if constexpr (L >= 4) acc_level<1>(hi, lo);
