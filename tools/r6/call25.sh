@@ -3,7 +3,7 @@
 # re-estimation
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r6/c25
+O=gpurun_out/r6/${C25:-c25}
 mkdir -p $O
 timeout -k 10 700 python -u -m pytest tests/test_gpu_tvl.py tests/test_gpu_edge.py tests/test_gpu_deferred.py tests/test_gpu_predict.py tests/test_gpu_estimate.py tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
 tail -2 $O/pytest.log
