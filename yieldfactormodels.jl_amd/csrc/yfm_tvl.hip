@@ -231,6 +231,8 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
     init_ok = r[kRecOk] != 0.0;
   }
   (void)Pc;
+  double l_minm = __builtin_inf();  // this lane's smallest maturity (the λ-overflow test below)
+  for (int i = j; i < N; i += L) l_minm = fmin(l_minm, s_mr[i].x);
   const double sigma2 = p.sigma2;
   const double rsig2 = 1.0 / sigma2;
 
@@ -312,11 +314,12 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
       const double lam = 1e-2 + exp(beta[3]);  // tvλdns.jl:56
       const double rl = 1.0 / lam;
       const double dl = lam - 1e-2;            // filter.jl:38
-      // λ near the FP64 range (c1 or c2 overflows): every z = e^{−λm} underflows to 0 and the
-      // reference's Jacobian column is ((β2+β3)·0 + β3·0)·dλ = 0·dλ (0, or NaN for dλ = Inf), so the
-      // factored form's constants become 0·dλ instead of multiplying z = 0 by an Inf
+      // λ near the FP64 range: every z = e^{−λm} of this lane underflows to 0 (λ·m_min > 746, or c1 or c2
+      // overflows) and the reference's Jacobian column is ((β2+β3)·0 + β3·0)·dλ = 0·dλ (0, or NaN for
+      // dλ = Inf), so the factored form's constants become 0·dλ instead of multiplying z = 0 by an Inf
+      // (c2·m can overflow with c2 itself finite: randomized sweep case 4985, λ = 3.6e304)
       const double c1r = (beta[1] + beta[2]) * dl, c2r = beta[2] * dl;
-      const bool big = !(fabs(c1r) <= __DBL_MAX__) || !(fabs(c2r) <= __DBL_MAX__);
+      const bool big = !(lam * l_minm <= 746.0) || !(fabs(c1r) <= __DBL_MAX__) || !(fabs(c2r) <= __DBL_MAX__);
       const double c1 = big ? 0.0 * dl : c1r;
       const double c2 = big ? 0.0 * dl : c2r;
       const double k1 = c1 * rl;

@@ -461,10 +461,11 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
       const dd lam = dd_add_d(e4, 1e-2);
       const dd dl = dd_add_d(lam, -1e-2);
       const dd rl = dd_rcp(lam);
-      // λ near the FP64 range: every z underflows to 0 and the reference's Jacobian column is 0·dλ
-      // (yfm_tvl.hip) — the constants become 0·dλ rather than overflowed (Inf, NaN) pairs
+      // λ near the FP64 range: every z of this lane underflows to 0 and the reference's Jacobian column is 0·dλ
+      // (yfm_tvl.hip) — the constants become 0·dλ rather than overflowed (Inf, NaN) pairs or a c2·m_max beyond the
+      // range (randomized sweep case 4985: λ = 3.6e304, c2 finite)
       const dd c1r = dd_mul(dd_add(beta[1], beta[2]), dl), c2r = dd_mul(beta[2], dl);
-      const bool big = !(fabs(c1r.hi) <= __DBL_MAX__) || !(fabs(c2r.hi) <= __DBL_MAX__);
+      const bool big = !(lam.hi * l_minm <= 746.0) || !(fabs(c1r.hi) <= __DBL_MAX__) || !(fabs(c2r.hi) <= __DBL_MAX__);
       const dd c1 = big ? dd_make(0.0 * dl.hi) : c1r;
       const dd c2 = big ? dd_make(0.0 * dl.hi) : c2r;
       const dd k1 = dd_mul(c1, rl);
