@@ -16,7 +16,8 @@ then closer to the truth than the oracle); YFM_SWEEP_REPORT=<file> appends one J
 
 The default suite runs seeds 0-11 plus every seed a 3,000-case sweep has ever failed (KNOWN_HARD:
 GNS5 with N ∈ {1, 3, 7, 12, 33, 64} and DNS with N = 1 — ill-conditioned or rank-deficient Z'Z,
-evaluated on the double-double capacitance path since round 3)."""
+evaluated on the double-double capacitance path since round 3) and 4985 (round 6).  TVλ cases are run a second
+time in the FP64 mode (`_check_tvl_fp64`: patterns exact, accuracy reported)."""
 from __future__ import annotations
 
 import ctypes
@@ -128,6 +129,37 @@ def test_random_cases_vs_c_oracle(engine, seed):
         e_or = abs(ref[b] - truth[b]) / max(abs(truth[b]), scale[b])
         assert e_gt <= e_or, (what, b, err[b], e_gt, e_or)
     assert not strict_fail, (what, strict_fail, got[strict_fail], ref[strict_fail], truth[strict_fail])
+    if kind == KIND_TVL:
+        _check_tvl_fp64(engine, Th, space, T_use, ref, truth, scale, what, seed)
+
+
+def _check_tvl_fp64(engine, Th, space, T_use, ref, truth, scale, what, seed):
+    """The TVλ FP64 mode (yfm_set_precision) on the same case: NaN pattern exact, and a −Inf that differs from the
+    FP64 oracle's agrees with the binary128 truth.  Its finite logliks are reported, not gated (YFM_SWEEP_REPORT):
+    the capacitance form's v'F⁻¹v = (v'v − u'Wu)/σ² cancels where the start is far from the data, so on such steps the
+    FP64 mode is less accurate than the reference's dense FP64 — the certified default is
+    the mode the factor-1 rule gates."""
+    from yfm_amd import _lib
+    old = engine.precision
+    engine.precision = _lib.PREC_FP64
+    try:
+        f = engine.loglik(KIND_TVL, Th, space=space, T_use=T_use)
+    finally:
+        engine.precision = old
+    assert np.array_equal(np.isnan(f), np.isnan(ref)), ("fp64", what)
+    assert not np.isposinf(f).any(), ("fp64", what)
+    for b in np.flatnonzero(np.isneginf(f) != np.isneginf(ref)):
+        assert np.isneginf(truth[b]) == np.isneginf(f[b]), ("fp64", what, b, f[b], ref[b], truth[b])
+    rep = os.environ.get("YFM_SWEEP_REPORT")
+    if rep:
+        import json
+        both = np.isfinite(f) & np.isfinite(truth) & np.isfinite(ref)
+        sc = np.maximum(np.abs(truth), np.where(np.isfinite(scale), scale, 0.0))
+        e64 = np.abs(f[both] - truth[both]) / np.maximum(sc[both], 1e-300)
+        eor = np.abs(ref[both] - truth[both]) / np.maximum(sc[both], 1e-300)
+        with open(rep, "a") as fh:
+            fh.write(json.dumps(dict(seed=seed, fp64=True, n=int(both.sum()), e64=[float(x) for x in e64],
+                                     e_oracle=[float(x) for x in eor])) + "\n")
 
 
 def engine_deferred(engine):

@@ -9,8 +9,18 @@ YFM_RANDOM_SEEDS=${SEEDS:-1000} YFM_SWEEP_REPORT=$O/sweep.jsonl timeout -k 10 10
 tail -3 $O/pytest.log
 python - <<PY
 import json
+import numpy as np
 rows = [json.loads(l) for l in open("$O/sweep.jsonl")]
-print("cases", len(rows), "finite candidates", sum(r["n"] for r in rows), "strict failures", sum(len(r["strict_fail"]) for r in rows),
-      "within only by term scale", sum(len(r["within_only_by_term_scale"]) for r in rows))
+cert = [r for r in rows if not r.get("fp64")]
+f64 = [r for r in rows if r.get("fp64")]
+print("cases", len(cert), "finite candidates", sum(r["n"] for r in cert), "strict failures", sum(len(r["strict_fail"]) for r in cert),
+      "within only by term scale", sum(len(r["within_only_by_term_scale"]) for r in cert))
+if f64:
+    e = np.array([x for r in f64 for x in r["e64"]]); o = np.array([x for r in f64 for x in r["e_oracle"]])
+    print("TVλ FP64 mode:", len(f64), "cases", e.size, "finite candidates; rel err vs truth median %.2e p99 %.2e max %.2e;"
+          " dense FP64 oracle median %.2e p99 %.2e max %.2e" % (np.median(e), np.quantile(e, 0.99), e.max(), np.median(o), np.quantile(o, 0.99), o.max()))
+    for th in (1e-12, 1e-9, 1e-6):
+        print("  > %.0e: FP64 mode %d, oracle %d" % (th, int((e > th).sum()), int((o > th).sum())))
+    print("  FP64 mode worse than 10x the oracle's error and > 1e-12:", int(((e > 10 * o) & (e > 1e-12)).sum()))
 PY
 exit $rc
