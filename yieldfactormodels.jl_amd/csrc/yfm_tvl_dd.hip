@@ -108,6 +108,12 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// the dd held by lane S of this lane's 16-lane row (DPP row_newbcast)
+template <int S>
+__device__ __forceinline__ dd row_bcast(dd x) {
+  return {quad_dpp<0x150 + S>(x.hi), quad_dpp<0x150 + S>(x.lo)};
+}
+
 template <int S>
 __device__ __forceinline__ void bcast_row(const dd (&v)[M4], dd (&out)[M4]) {
 #pragma unroll
@@ -130,7 +136,12 @@ __device__ __forceinline__ void gather_sym(const dd (&col)[M4], dd (&X)[M4][M4])
 // xch: this filter's 4×4 dd exchange block in LDS (the transpose of the new P's columns).  The transpose by quad DPP
 // exchanges instead (no wave barriers) measured slower even at L = 64, where the step is latency-bound (B = 1: 7.30 vs
 // 7.15 ms; profiles/r6/tvl_latency/run1): a dd lane-dependent select costs more than the barrier it removes.
-__device__ __forceinline__ void dd_propagate_q(const double* par, int qr, const dd (&b)[M4], const dd (&xc)[M4],
+// SPLIT (L ≥ 16: four quads per 16-lane row, qg = the quad's index in its row): lane (qr, qg) forms only entry qg
+// of column qr of A and entry qg of column qr of the new P — the same operations in the same order as the role's full
+// column, so the result is bitwise the unsplit one — and row qg of A comes from its own quad (one quad broadcast per
+// entry instead of the 4×4 gather).  A quarter of the propagation's products per lane on the latency-bound wide groups.
+template <bool SPLIT>
+__device__ __forceinline__ void dd_propagate_q(const double* par, int qr, int qg, const dd (&b)[M4], const dd (&xc)[M4],
                                                bool scale, dd* xch, dd (&beta)[M4], dd (&Pc)[M4]) {
   const dd* Phi = reinterpret_cast<const dd*>(par + kDPhi);
   const dd* Q = reinterpret_cast<const dd*>(par + kDQ);
@@ -143,6 +154,31 @@ __device__ __forceinline__ void dd_propagate_q(const double* par, int qr, const 
     beta[1] = quad_bcast<1>(s);
     beta[2] = quad_bcast<2>(s);
     beta[3] = quad_bcast<3>(s);
+  }
+  if constexpr (SPLIT) {
+    dd ac;
+    {
+      dd_acc a;
+#pragma unroll
+      for (int l = 0; l < M4; ++l) a.add_prod(Phi[qg * M4 + l], xc[l]);
+      ac = a.value();  // A[qg][qr]
+    }
+    const dd ar[M4] = {quad_bcast<0>(ac), quad_bcast<1>(ac), quad_bcast<2>(ac), quad_bcast<3>(ac)};  // row qg of A
+    dd pc;
+    {
+      dd_acc a;
+#pragma unroll
+      for (int l = 0; l < M4; ++l) a.add_prod(ar[l], Phi[qr * M4 + l]);
+      dd s = a.value();
+      if (scale) s = dd_mul(s, sig2);
+      pc = dd_add(s, Q[qg <= qr ? utri(qg, qr) : utri(qr, qg)]);
+    }
+    xch[qr * M4 + qg] = pc;
+    wave_sync();
+#pragma unroll
+    for (int k = 0; k < M4; ++k) Pc[k] = xch[k <= qr ? qr * M4 + k : k * M4 + qr];
+    wave_sync();  // the block is rewritten by the next exchange
+    return;
   }
   dd At[M4][M4];  // At[l][i] = A[i][l]
   {
@@ -371,6 +407,8 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
 
   // the 4×4 update is distributed over the lanes of each quad: role qr holds column qr of P
   const int qr = tid & 3;
+  constexpr bool SPLIT = L >= 16;  // the 4×4 update's entries spread over the four quads of a 16-lane row
+  const int qg = (tid >> 2) & 3;
   constexpr int kUnrollK1 = LONG ? 2 : 1;  // the one-jump maturity loop (below)
   constexpr bool FACT = L <= 8;              // 1/λ factored out of the z2 sums (below)
   dd* xch = s_xch + grp * kXchStride;
@@ -449,7 +487,7 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
         bf[i] = beta[i];
         xc[i] = Pc[i];
       }
-      dd_propagate_q(par, qr, bf, xc, false, xch, beta, Pc);
+      dd_propagate_q<SPLIT>(par, qr, qg, bf, xc, false, xch, beta, Pc);
       if (acc) {
         sum_ld.add(dd_make(last_ld));
         sum_q.add(dd_make(last_q));
@@ -607,8 +645,21 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
       } else {
         for (int i = j; i < N; i += L) accum(s_m[i], col[i], s_rm[i], dd_exp(neg_rate(lam, s_m[i])));
       }
-      dd s2 = group_sum_acc<L>(S2), g22 = group_sum_acc<L>(G22), g2z = group_sum_acc<L>(G2z);
-      dd g24 = group_sum_acc<L>(G24), y2 = group_sum_acc<L>(Y2);
+      dd s2, g22, g2z, g24, y2, sz, s4, gzz, gz4, g44, yz, y4;
+      if constexpr (L >= 16) {
+        // recursive halving (yfm_dd.hpp group_sum12): bitwise the butterfly's sums at about half its cost
+        const dd_acc in[12] = {S2, G22, G2z, G24, Y2, Sz, S4, Gzz, Gz4, G44, Yz, Y4};
+        dd o[12];
+        group_sum12<L>(in, o);
+        s2 = o[0]; g22 = o[1]; g2z = o[2]; g24 = o[3]; y2 = o[4];
+        sz = o[5]; s4 = o[6]; gzz = o[7]; gz4 = o[8]; g44 = o[9]; yz = o[10]; y4 = o[11];
+      } else {
+        s2 = group_sum_acc<L>(S2); g22 = group_sum_acc<L>(G22); g2z = group_sum_acc<L>(G2z);
+        g24 = group_sum_acc<L>(G24); y2 = group_sum_acc<L>(Y2);
+        sz = group_sum_acc<L>(Sz); s4 = group_sum_acc<L>(S4);
+        gzz = group_sum_acc<L>(Gzz); gz4 = group_sum_acc<L>(Gz4); g44 = group_sum_acc<L>(G44);
+        yz = group_sum_acc<L>(Yz); y4 = group_sum_acc<L>(Y4);
+      }
       if constexpr (FACT) {
         const dd rl2 = dd_mul(rl, rl);
         s2 = dd_mul(s2, rl);
@@ -617,9 +668,6 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
         g24 = dd_mul(g24, rl);
         y2 = dd_mul(y2, rl);
       }
-      const dd sz = group_sum_acc<L>(Sz), s4 = group_sum_acc<L>(S4);
-      const dd gzz = group_sum_acc<L>(Gzz), gz4 = group_sum_acc<L>(Gz4), g44 = group_sum_acc<L>(G44);
-      const dd yz = group_sum_acc<L>(Yz), y4 = group_sum_acc<L>(Y4);
       // back to the loading basis (1, z2, z3 = z2 − z, z4)
       const dd g23 = dd_sub(g22, g2z);
       dd G[M4][M4];
@@ -662,7 +710,25 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
       // role qr forms row qr of B̃ (P symmetric: its row qr is the column it holds), every lane
       // factorises the broadcast B̃ and solves for ONE right-hand side, column qr of P ----
       dd A[M4][M4];
-      {
+      if constexpr (SPLIT) {
+        // lane (qr, qg): entry (qr, qg) of B̃ (the unsplit role's Ar[qg], same operations); entry (r, k) is in lane 4k + r
+        // of the row
+        dd_acc a;
+        a.add(qg == qr ? sig2 : dd_make(0.0));
+#pragma unroll
+        for (int l = 0; l < M4; ++l) {
+          // G[l][qg] by a bit mux on the two halves (a select of dd values becomes a scratch-indexed load)
+          const bool b0 = (qg & 1) != 0, b1 = (qg & 2) != 0;
+          const double h = b1 ? (b0 ? G[l][3].hi : G[l][2].hi) : (b0 ? G[l][1].hi : G[l][0].hi);
+          const double o = b1 ? (b0 ? G[l][3].lo : G[l][2].lo) : (b0 ? G[l][1].lo : G[l][0].lo);
+          a.add_prod(Pc[l], dd{h, o});
+        }
+        const dd ar = a.value();
+        A[0][0] = row_bcast<0>(ar); A[1][0] = row_bcast<1>(ar); A[2][0] = row_bcast<2>(ar); A[3][0] = row_bcast<3>(ar);
+        A[0][1] = row_bcast<4>(ar); A[1][1] = row_bcast<5>(ar); A[2][1] = row_bcast<6>(ar); A[3][1] = row_bcast<7>(ar);
+        A[0][2] = row_bcast<8>(ar); A[1][2] = row_bcast<9>(ar); A[2][2] = row_bcast<10>(ar); A[3][2] = row_bcast<11>(ar);
+        A[0][3] = row_bcast<12>(ar); A[1][3] = row_bcast<13>(ar); A[2][3] = row_bcast<14>(ar); A[3][3] = row_bcast<15>(ar);
+      } else {
         dd Ar[M4];
 #pragma unroll
         for (int k = 0; k < M4; ++k) {
@@ -711,7 +777,7 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
       const double dh = dd_to_double(det);
       const bool upd = dh != 0.0;  // inv(F) threw: return without updating (filter.jl:51-56)
       if (upd) {
-        dd_propagate_q(par, qr, bf, ws, true, xch, beta, Pc);
+        dd_propagate_q<SPLIT>(par, qr, qg, bf, ws, true, xch, beta, Pc);
       }
       last_ld = upd ? log(fabs(dh)) : -__builtin_inf();
       last_q = upd ? q : __builtin_nan("");
