@@ -894,7 +894,7 @@ int tvl_dd_lanes_for(int B, int N, int want, int share) {
   // The L with the least modelled time.  The kernel needs the whole register file (one wave per SIMD, 1,024 on the
   // chip), so waves run in rounds of 1,024; per filter step a wave issues ≈ ⌈N/L⌉·137 instructions of maturity loop,
   // ≈ 4,250 of 4×4 dd update and per-step constants (replicated on every quad of a group) and ≈ 200 per butterfly
-  // level (instruction counts of this build's ISA).  `share` concurrent launches of this size divide the SIMDs.
+  // level (instruction counts of this build's ISA; L ≥ 16 below).  `share` concurrent launches of this size divide the SIMDs.
   // Measured choices it keeps at N = 360: B = 16,384 → 4, B ≤ 1,024 → 64 (profiles/r5/first/c3_B*_L*.json).  At
   // N = 30 the update dominates: the estimator's 7,680-point rounds (two at once) take L = 4, where the round-5
   // rule ("one wave per SIMD of lanes") gave 16 — four rounds of waves instead of one.
@@ -903,7 +903,11 @@ int tvl_dd_lanes_for(int B, int N, int want, int share) {
   double best_cost = 0.0;
   for (int L = 4, lg = 2; L <= capN; L <<= 1, ++lg) {
     const double rounds = std::ceil(waves_unit * L / 1024.0);
-    const double issue = (double)((N + L - 1) / L) * 137.0 + 4250.0 + 200.0 * lg;
+    // L ≥ 16: the update's products split over the four quads of a row and the sums by recursive halving
+    // (group_sum12): ≈ 3,650 + 288 + 60 per level after the second (B = 1 at L = 64: 6.48 → 5.17 ms, L = 16 at
+    // B = 4,096: 8.97 → 7.84 ms, profiles/r6/tvl_latency/c29b/)
+    const double issue = (double)((N + L - 1) / L) * 137.0 +
+                         (L >= 16 ? 3650.0 + 288.0 + 60.0 * (lg - 2) : 4250.0 + 200.0 * lg);
     const double cost = rounds * issue;
     if (L == 4 || cost < best_cost) {
       best = L;
