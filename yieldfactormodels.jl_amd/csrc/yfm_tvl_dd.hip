@@ -685,14 +685,35 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
       // u_c = Σ_i Z_ic (y_i − ŷ_i), ŷ = β1 + β2 z2 + β3 z3;  v'v = y'y − β'(Z'y)[1:3] − β'u[1:3]
       const dd sy = s_sum[kSumDd * tt], syy = s_sum[kSumDd * tt + 1];
       const dd zy[M4] = {sy, y2, y3, y4};
+      // entry qg of a row of 4 dd values held in every lane (a bit mux on the halves: a select of dd values becomes a
+      // scratch-indexed load)
+      const bool qb0 = (qg & 1) != 0, qb1 = (qg & 2) != 0;
+      auto selq4 = [qb0, qb1](dd v0, dd v1, dd v2, dd v3) {
+        const double h = qb1 ? (qb0 ? v3.hi : v2.hi) : (qb0 ? v1.hi : v0.hi);
+        const double o = qb1 ? (qb0 ? v3.lo : v2.lo) : (qb0 ? v1.lo : v0.lo);
+        return dd{h, o};
+      };
       dd u[M4];
-#pragma unroll
-      for (int c = 0; c < M4; ++c) {
+      if constexpr (SPLIT) {
+        // lane (qr, qg) forms u[qg] (the same operations), u[c] is then read from lane 4c of the row
         dd_acc a;
-        a.add(zy[c]);
+        a.add(selq4(sy, y2, y3, y4));
 #pragma unroll
-        for (int l = 0; l < 3; ++l) a.add_prod(dd_neg(beta[l]), G[c][l]);
-        u[c] = a.value();
+        for (int l = 0; l < 3; ++l) a.add_prod(dd_neg(beta[l]), selq4(G[l][0], G[l][1], G[l][2], G[l][3]));  // G[qg][l]
+        const dd uq = a.value();
+        u[0] = row_bcast<0>(uq);
+        u[1] = row_bcast<4>(uq);
+        u[2] = row_bcast<8>(uq);
+        u[3] = row_bcast<12>(uq);
+      } else {
+#pragma unroll
+        for (int c = 0; c < M4; ++c) {
+          dd_acc a;
+          a.add(zy[c]);
+#pragma unroll
+          for (int l = 0; l < 3; ++l) a.add_prod(dd_neg(beta[l]), G[c][l]);
+          u[c] = a.value();
+        }
       }
       dd vv;
       {
@@ -716,13 +737,7 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
         dd_acc a;
         a.add(qg == qr ? sig2 : dd_make(0.0));
 #pragma unroll
-        for (int l = 0; l < M4; ++l) {
-          // G[l][qg] by a bit mux on the two halves (a select of dd values becomes a scratch-indexed load)
-          const bool b0 = (qg & 1) != 0, b1 = (qg & 2) != 0;
-          const double h = b1 ? (b0 ? G[l][3].hi : G[l][2].hi) : (b0 ? G[l][1].hi : G[l][0].hi);
-          const double o = b1 ? (b0 ? G[l][3].lo : G[l][2].lo) : (b0 ? G[l][1].lo : G[l][0].lo);
-          a.add_prod(Pc[l], dd{h, o});
-        }
+        for (int l = 0; l < M4; ++l) a.add_prod(Pc[l], selq4(G[l][0], G[l][1], G[l][2], G[l][3]));
         const dd ar = a.value();
         A[0][0] = row_bcast<0>(ar); A[1][0] = row_bcast<1>(ar); A[2][0] = row_bcast<2>(ar); A[3][0] = row_bcast<3>(ar);
         A[0][1] = row_bcast<4>(ar); A[1][1] = row_bcast<5>(ar); A[2][1] = row_bcast<6>(ar); A[3][1] = row_bcast<7>(ar);
