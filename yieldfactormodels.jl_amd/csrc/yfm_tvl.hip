@@ -81,6 +81,13 @@ __global__ __launch_bounds__(256) void tvl_init_kernel(const double* __restrict_
   r[47] = 0.0;
 }
 
+// x of lane `src` of this wave (ds_bpermute: the LDS crossbar, no LDS memory and no wave barrier)
+__device__ __forceinline__ double lane_read_f64(int src, double x) {
+  const int lo = __builtin_amdgcn_ds_bpermute(src << 2, __double2loint(x));
+  const int hi = __builtin_amdgcn_ds_bpermute(src << 2, __double2hiint(x));
+  return __hiloint2double(hi, lo);
+}
+
 // Lane-distributed 4×4 update (L ≥ 4): the four roles qr = lane & 3 of each quad hold column qr of P,
 // row qr of Φ, column qr of Q and δ_qr; the group's other quads repeat the same work.  Every
 // quantity is formed with the replicated kernel's operation order, so the results are bitwise
@@ -89,6 +96,8 @@ __global__ __launch_bounds__(256) void tvl_init_kernel(const double* __restrict_
 // the group's LDS exchange block).
 struct TvlQuad {
   int qr;
+  int qg;              // L ≥ 16: this quad's index in its 16-lane row
+  double phq[4], qcq;  // L ≥ 16: row qg of Φ, Q[qg][qr]
   double phr[4], qc[4], dq;
   double phi[4][4];  // Φ (every row: column qr of Φ Pf)
   double* xch;  // this group's 4×4 exchange block (LDS)
@@ -125,6 +134,22 @@ struct TvlQuad {
     beta[1] = quad_bcast_f64<1>(bq);
     beta[2] = quad_bcast_f64<2>(bq);
     beta[3] = quad_bcast_f64<3>(bq);
+    if constexpr (DPP) {
+      // L ≥ 16: lane (qr, qg) forms entry qg of column qr of A and of the new P (role qr's ac[qg] and pc[qg], the
+      // same operations); row qg of A comes from its own quad, and column qr of the new P from the lanes that formed
+      // it (ds_bpermute) — a quarter of the products, four broadcasts instead of the sixteen of the 4×4 gather
+      double a = 0.0;
+#pragma unroll
+      for (int l = 0; l < 4; ++l) a = fma(phq[l], pf[l], a);
+      const double ar[4] = {quad_bcast_f64<0>(a), quad_bcast_f64<1>(a), quad_bcast_f64<2>(a), quad_bcast_f64<3>(a)};
+      double t = qcq;
+#pragma unroll
+      for (int l = 0; l < 4; ++l) t = fma(ar[l], phr[l], t);
+      const int base = (int)(threadIdx.x & 63) & ~15;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) Pc[k] = lane_read_f64(base + (k <= qr ? 4 * k + qr : 4 * qr + k), t);
+      return;
+    }
     double ac[4], At[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -197,6 +222,7 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
   if constexpr (DIST) {
     const double* r = rec + (size_t)bb * kRecLen;
     qd.qr = tid & 3;
+    qd.qg = (tid >> 2) & 3;
     qd.xch = s_xch + grp * 16;
     qd.dq = r[kRecDelta + qd.qr];
     p.sigma2 = r[kRecSigma];
@@ -210,6 +236,12 @@ __global__ __launch_bounds__(kTvlBlock, 2) void tvl_loglik_kernel(
       const int q = lo * M - lo * (lo - 1) / 2 + (hi - lo);  // upper-triangle record index
       qd.qc[i] = r[kRecQ + q];
       Pc[i] = r[kRecP + q];
+    }
+#pragma unroll
+    for (int l = 0; l < M; ++l) qd.phq[l] = r[kRecPhi + qd.qg * M + l];
+    {
+      const int lo = qd.qg < qd.qr ? qd.qg : qd.qr, hi = qd.qg < qd.qr ? qd.qr : qd.qg;
+      qd.qcq = r[kRecQ + lo * M - lo * (lo - 1) / 2 + (hi - lo)];
     }
     init_ok = r[kRecOk] != 0.0;
   } else {
