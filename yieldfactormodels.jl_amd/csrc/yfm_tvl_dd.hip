@@ -579,9 +579,24 @@ __global__ __launch_bounds__(kDdBlock, 1) void tvl_dd_loglik_kernel(
         if (pstep > 0.0) {
           // power mode: one dd exp, b = e^{−λΔ}; the lane's start value and the group's jump factors are integer
           // powers of it (m_j/Δ and e_q are exact integers) — in place of one dd exp per maturity
+          // The squarings b^(2^k) are formed once per step and shared by the lane's powers (dd_powi squares again in
+          // every call): each power is then the same products of the same factors in the same order — bitwise
+          // dd_powi's — at one dd product per set bit (jump exponents < 512: the host's power table)
           const dd bs = dd_exp(neg_rate(lam, pstep));
-          z = (j < N) ? dd_powi(bs, (int)(s_m[j] / pstep)) : dd_make(0.0);
-          for (int q = j; q < K; q += L) w[q] = dd_powi(bs, (int)s_gd[q]);
+          dd sq[9];
+          sq[0] = bs;
+#pragma unroll
+          for (int k = 1; k < 9; ++k) sq[k] = dd_mul(sq[k - 1], sq[k - 1]);
+          auto pow_sq = [&](int n) {
+            dd r = dd_make(1.0);
+#pragma unroll
+            for (int k = 0; k < 9; ++k)
+              if ((n >> k) & 1) r = dd_mul(r, sq[k]);
+            return r;
+          };
+          const int n0 = (int)(s_m[j] / pstep);
+          z = (j < N) ? (n0 < 512 ? pow_sq(n0) : dd_powi(bs, n0)) : dd_make(0.0);
+          for (int q = j; q < K; q += L) w[q] = pow_sq((int)s_gd[q]);
         } else {
           z = (j < N) ? dd_exp(neg_rate(lam, s_m[j])) : dd_make(0.0);
           // a jump equal to some lane's first maturity (uniform grids: d = L·Δ = m_{L−1}) is that
