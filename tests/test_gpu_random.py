@@ -28,7 +28,7 @@ import pytest
 
 from conftest import ROOT
 from oracle import kalman_ld as LD
-from oracle.truth import loglik_truth, predict_states_truth
+from oracle.truth import loglik_truth, predict_states_truth, states_truth
 from yfm_amd import KIND_DNS, KIND_GNS, KIND_TVL
 from yfm_amd import synthetic as S
 from yfm_amd.params import n_params, transform_params
@@ -166,7 +166,7 @@ def engine_deferred(engine):
     return engine.last_deferred()
 
 
-@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("seed", range(int(os.environ.get("YFM_TRAJ_SEEDS", "6"))))  # a wider sweep on demand
 def test_random_trajectories_vs_oracle(engine, seed):
     """predict (NaN-padded horizon, ragged windows) and get_loss_array on random shapes vs the NumPy
     oracle (filter.jl:211-282): normwise 1e-9 per output array; NaN / −Inf patterns exact."""
@@ -193,17 +193,26 @@ def test_random_trajectories_vs_oracle(engine, seed):
         O.set_params(s, Th[:, b])
         ref = O.predict(s, O.pad_nan(Y[:, :tu[b]], h))
         n = tu[b] + h - 1
-        if kind == KIND_TVL:  # EKF: adjudicated by the binary128 trajectory (tests/test_gpu_predict.py)
-            from test_gpu_predict import assert_close_truth
-            A = predict_states_truth(kind, Y[:, :tu[b]], mats, Th[:, b], horizon=h)[:n + 1]
+        # factors and predictions: within 1e-9 of the FP64 oracle or at least as close to the binary128 trajectory
+        # (tests/test_gpu_predict.py: assert_close_truth) — every kind: a 600-seed sweep found DNS / GNS5 cases
+        # (N = 3 with M = 5, near-singular starts) where the FP64 oracle itself is more than 1e-9 off
+        from test_gpu_predict import assert_close_truth
+        A = predict_states_truth(kind, Y[:, :tu[b]], mats, Th[:, b], horizon=h)[:n + 1]
+        if kind == KIND_TVL:
             tru = {"factors": A[1:].T, "preds": LD.fitted_tvl(mats, A[:n]).T}
-            for k in ("factors", "preds"):
+        else:
+            s = O.KalmanState.fresh(kind, mats, state_dim(kind))
+            O.set_params(s, Th[:, b])
+            tru = {"factors": A[1:].T, "preds": s.Z @ A[:n].T}
+        fin_traj = np.isfinite(ref["factors"]).any()
+        for k in ("factors", "preds"):
+            if fin_traj:
                 assert_close_truth(r[k][:, :n, b], ref[k], tru[k], what=(seed, k, b))
         for k, v in ref.items():
             got = r[k][:, :n, b]
             assert np.array_equal(np.isnan(got), np.isnan(v)), (seed, k, b)
             fin = np.isfinite(v)
-            if fin.any() and kind != KIND_TVL:
+            if fin.any() and kind != KIND_TVL and k not in ("factors", "preds"):  # γ and the fixed loadings
                 sc = max(np.abs(v[fin]).max(), 1e-300)
                 assert np.abs(got[fin] - v[fin]).max() / sc <= 1e-9, (seed, k, b, N, T)
             assert np.isnan(r[k][:, n:, b]).all()
@@ -213,6 +222,15 @@ def test_random_trajectories_vs_oracle(engine, seed):
         got_la = la[:tu[b] - 1, b]
         if np.isscalar(ref_la):
             assert np.isneginf(got_la).all() or got_la.size == 0, (seed, b)
-        elif kind != KIND_TVL:
-            sc = max(np.abs(ref_la).max(), 1e-300) if ref_la.size else 1.0
-            assert np.abs(got_la - ref_la).max(initial=0.0) / sc <= 1e-9, (seed, b)
+        elif kind != KIND_TVL and ref_la.size:
+            # −v'v/N per step (filter.jl:211-247) from the binary128 states: v_t = y_t − Z β_{t|t−1}
+            _, Bt, _ = states_truth(kind, Y[:, :tu[b]], mats, Th[:, b], space=1)
+            tru_la = np.zeros(tu[b] - 1)
+            for t in range(2, tu[b]):
+                v = Y[:, t - 1] - s.Z @ Bt[:, t - 2]
+                tru_la[t - 1] = -float(v @ v) / N
+            sc = max(np.abs(tru_la).max(), 1e-300)
+            e_go = np.abs(got_la - ref_la).max(initial=0.0) / sc
+            e_gt = np.abs(got_la - tru_la).max(initial=0.0) / sc
+            e_or = np.abs(ref_la - tru_la).max(initial=0.0) / sc
+            assert e_go <= 1e-9 or e_gt <= e_or, (seed, b, e_go, e_gt, e_or)
